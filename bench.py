@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s and ms/frame at 1 spp per frame (BASELINE.json metric).
+
+A step is one progressive frame (one display() of OpenglRayTracing/main.cpp:558-603)
+of the configured workload: 1 spp for every pixel of the frame, running-mean
+accumulate, and for N > 1 ranks the RCCL gather of every rank's screen-tile
+shard to rank 0 (bit-exact reassembly). Default workload: configs[1] = c2,
+the OpenglRayTracing bunny scene (5k tris) at 1920x1080, Lambert, 2 bounces.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (driver launch for N > 1)
+
+Rank 0 prints one JSON line (contract in the task statement), with
+``roofline`` (algorithmic bytes of the reference algorithm per launch / the
+kernel's HIP-event duration, against the 8 TB/s HBM peak) and ``cpu_baseline``
+(the CPU restatement of the reference on the host cores, rank 0 at N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "Mrays/sec + ms/frame (1 spp, 1080p) at 1/2/4/8 MI355X; CPU-ref spp-matched PSNR"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--builder", default=None, help="override the config's BVH builder")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=2, help="cpu_baseline sample: full frames rendered")
+    ap.add_argument("--traffic", default=None, help="JSON file with per-launch PMC HBM bytes (profiles/)")
+    ap.add_argument("--flags", type=int, default=0)
+    return ap.parse_args()
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_env()
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
+    n = world
+
+    from opengl_ray_tracing_amd import FLAG_COUNT_FETCHES, Renderer, orbit_camera, scenes
+
+    cfg, tris, nodes, hdr = scenes.build_config(args.config, args.builder)
+    eye, rot = orbit_camera(*cfg.camera)
+
+    torch = None
+    if n > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+
+    r = Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=local,
+                 tile_rank=rank, tile_world=n, flags=args.flags)
+    r.upload_scene(tris, nodes)
+    r.upload_env(hdr)
+
+    # ---- algorithmic bytes per ray of the reference algorithm, counted on the GPU by the
+    # instrumented kernel variant (no culling, closest-hit shadows: exactly pass1.fsh's fetches)
+    rc = Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=local,
+                  tile_rank=rank, tile_world=n, flags=FLAG_COUNT_FETCHES)
+    rc.upload_scene(tris, nodes)
+    rc.upload_env(hdr)
+    rc.render_frame(eye, rot, 0)
+    cs = rc.stats()
+    rc.close()
+    bytes_per_ray = (48 * cs.node_fetch + 72 * cs.tri_fetch + 72 * cs.mat_fetch + 12 * cs.tex_fetch) / max(cs.rays, 1)
+
+    # ---- multi-GPU gather buffers (screen-tile shards)
+    if n > 1:
+        counts = [r.owned_pixel_count(k, n) for k in range(n)]
+        maxc = max(counts)
+        send = torch.zeros((maxc, 4), dtype=torch.float32, device=f"cuda:{local}")
+        gather = [torch.zeros((maxc, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n)] \
+            if rank == 0 else None
+        stream = torch.cuda.current_stream().cuda_stream
+        r.set_stream(stream)
+
+    def step(frame):
+        r.render_frame(eye, rot, frame, sync=False)
+        if n > 1:
+            r.pack_owned(send.data_ptr())
+            dist.gather(send, gather_list=gather, dst=0)
+            if rank == 0:
+                for k in range(1, n):
+                    r.unpack_rank(k, n, gather[k].data_ptr())
+
+    def sync_all():
+        r.synchronize()
+        if n > 1:
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for f in range(args.warmup):
+        step(f)
+    sync_all()
+    r.reset_stats()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    sync_all()
+    t1 = time.perf_counter()
+    st = r.stats()
+
+    elapsed = t1 - t0
+    rays_local = st.rays
+    if n > 1:
+        tt = torch.tensor([elapsed, float(rays_local), st.kernel_ms_total], dtype=torch.float64, device=f"cuda:{local}")
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0].item())
+        rays_total = float(sm[1].item())
+        kernel_ms_avg = float(mx[2].item()) / max(st.launches, 1)
+    else:
+        rays_total = float(rays_local)
+        kernel_ms_avg = st.kernel_ms_total / max(st.launches, 1)
+
+    if rank == 0:
+        ms_per_step = 1e3 * elapsed / args.steps
+        mrays = rays_total / elapsed / 1e6
+        rays_per_launch = rays_local / max(st.launches, 1)
+        achieved = rays_per_launch * bytes_per_ray / (kernel_ms_avg * 1e-3) / 1e9
+        traffic = None
+        if args.traffic and Path(args.traffic).exists():
+            traffic = json.loads(Path(args.traffic).read_text()).get(args.config)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "renderKernel<%s>" % cfg.integrator, "kernel_ms": round(kernel_ms_avg, 4),
+                    "bytes_per_ray": round(bytes_per_ray, 1), "rays_per_launch": int(rays_per_launch)}
+        cpu = None
+        if not args.no_cpu_baseline and n == 1:
+            cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_frames)
+        line = {
+            "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{cfg.name}: {cfg.description}", "resolution": f"{cfg.width}x{cfg.height}",
+                       "spp_per_frame": 1, "integrator": cfg.integrator, "max_bounce": cfg.max_bounce,
+                       "triangles": int(tris.shape[0]), "bvh_nodes": int(nodes.shape[0]),
+                       "bvh_builder": args.builder or cfg.builder, "env": cfg.env,
+                       "parallelism": f"screen-tile x{n}" + (" + RCCL gather" if n > 1 else "")},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    r.close()
+    if n > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, frames):
+    """The CPU restatement of the reference (oracle/, test infrastructure) timed on the host
+    cores: `frames` full frames of the same workload, OpenMP over pixels."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle  # noqa: E402  (bench.py's cpu_baseline leg is the only bench use of oracle/)
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    orc = oracle.Oracle(tris, nodes, hdr)
+    acc = np.zeros((cfg.height, cfg.width, 4), np.float32)
+    rays = 0
+    t0 = time.perf_counter()
+    for f in range(frames):
+        acc, c = orc.render(cfg.width, cfg.height, cfg.integrator, f, eye, rot, accum=acc,
+                            max_bounce=cfg.max_bounce, threads=cores)
+        rays += c.rays
+    dt = time.perf_counter() - t0
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"{frames} full {cfg.width}x{cfg.height} frames of {cfg.name} ({rays} rays, {dt:.1f} s)",
+            "ms_per_frame": round(1e3 * dt / frames, 1)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,149 @@
+/*
+ * pt_abi.h -- C-ABI drop-in boundary of the MI355X progressive path tracer.
+ *
+ * The reference has no plugin/FFI API; its de-facto boundary is the GL
+ * contract around pass1.draw() (OpenglRayTracing/main.cpp:558-603,
+ * DisneyBRDF/main.cpp:558-603, ImportanceSampling_LowDiscrepancySequence/
+ * main.cpp:659-709). Each entry point below replaces one piece of that
+ * contract; the reference call it replaces is cited on each declaration.
+ *
+ * Conventions
+ *  - Return codes: 0 = OK, negative = PT_E_* (no exit(), unlike the reference's
+ *    exit(-1) at OpenglRayTracing/main.cpp:175,214,225,269).
+ *  - The caller owns host arrays; the library owns device buffers.
+ *  - One host thread per pt_ctx; calls are stream-ordered and synchronous on
+ *    return unless the name ends in _async.
+ *  - Images are row-major, row 0 = the bottom row (GL window coordinates,
+ *    pass1.fsh pix.y) for the GL integrators, row 0 = the top row for
+ *    PT_BASIC_CPU_COMPAT (BasicRayTracingWithC++/main.cpp:364-370).
+ */
+#ifndef PT_ABI_H
+#define PT_ABI_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+/* error codes */
+#define PT_OK 0
+#define PT_E_INVALID -1      /* bad argument */
+#define PT_E_HIP -2          /* HIP runtime error (see pt_last_error) */
+#define PT_E_NOSCENE -3      /* render before pt_upload_scene */
+#define PT_E_BADSCENE -4     /* malformed node / triangle arrays */
+#define PT_E_NOMEM -5
+#define PT_E_IO -6           /* file open / parse failure */
+#define PT_E_NODEVICE -7     /* no HIP device / extension missing */
+
+/* integrators (one per reference kernel variant) */
+#define PT_LAMBERT_O 0            /* OpenglRayTracing/shaders/pass1.fsh: Lambert, uniform hemisphere, 2 bounces */
+#define PT_DISNEY_UNIFORM_D 1     /* DisneyBRDF/shaders/pass1.fsh: aniso Disney, uniform hemisphere, 5 bounces */
+#define PT_DISNEY_MIS_SOBOL_IS 2  /* ImportanceSampling_LowDiscrepancySequence/shaders/pass1.fsh: MIS + Sobol, 2 bounces */
+#define PT_BASIC_CPU_COMPAT 3     /* BasicRayTracingWithC++/main.cpp: spheres+triangles, RR 0.8, depth 8 */
+
+/* flags */
+#define PT_FLAG_NO_CULL 0x1u      /* traverse exactly like pass1.fsh:335-382 (no closest-t culling) */
+#define PT_FLAG_CLOSEST_SHADOW 0x2u /* env shadow rays use closest-hit instead of any-hit */
+#define PT_FLAG_COUNT_FETCHES 0x4u /* count reference-algorithm fetches (implies NO_CULL, closest shadow) */
+
+typedef struct pt_config {
+  int width;          /* RenderPass::width  (OpenglRayTracing/main.cpp:83), e.g. 1920 */
+  int height;         /* RenderPass::height (OpenglRayTracing/main.cpp:84), e.g. 1080 */
+  int integrator;     /* PT_LAMBERT_O .. PT_BASIC_CPU_COMPAT */
+  int max_bounce;     /* -1 = the reference's default for the integrator */
+  int device_id;      /* HIP device ordinal */
+  int tile_rank;      /* screen-tile shard owned by this context: tiles t with t % tile_world == tile_rank */
+  int tile_world;     /* 1 = whole frame */
+  int tile_size;      /* shard tile edge in pixels (0 = 32) */
+  uint32_t flags;     /* PT_FLAG_* */
+  int basic_samples;  /* PT_BASIC_CPU_COMPAT: SAMPLE (BasicRayTracingWithC++/main.cpp:17), 0 = 128 */
+  uint32_t basic_seed;/* PT_BASIC_CPU_COMPAT: seed of the per-pixel counter RNG */
+} pt_config;
+
+/* Counters accumulate over every launch since pt_create / pt_reset_stats. */
+typedef struct pt_frame_stats {
+  uint64_t rays;        /* hitBVH invocations (primary + BRDF + env shadow) */
+  uint64_t node_fetch;  /* PT_FLAG_COUNT_FETCHES only: getBVHNode calls (48 B) */
+  uint64_t tri_fetch;   /* PT_FLAG_COUNT_FETCHES only: getTriangle calls (72 B) */
+  uint64_t mat_fetch;   /* PT_FLAG_COUNT_FETCHES only: getMaterial calls (72 B) */
+  uint64_t tex_fetch;   /* PT_FLAG_COUNT_FETCHES only: texel reads (12 B) */
+  float kernel_ms;      /* device time of the last render launch (HIP events on its stream) */
+  float kernel_ms_total;/* summed device time of the render launches since the reset */
+  int launches;         /* render launches since the reset */
+  int max_stack;        /* traversal stack bound used (tree depth + 1) */
+} pt_frame_stats;
+
+typedef struct pt_ctx pt_ctx;
+
+/* Device selection, resolution, integrator (replaces glutInit/glewInit/RenderPass
+ * setup, OpenglRayTracing/main.cpp:639-644,749-768). */
+int pt_create(pt_ctx** out, const pt_config* cfg);
+void pt_destroy(pt_ctx* ctx);
+const char* pt_last_error(pt_ctx* ctx);  /* ctx may be NULL: last create error */
+int pt_device_count(int* n);
+
+/* Upload the encoded scene (replaces the two GL_RGB32F texture buffers,
+ * OpenglRayTracing/main.cpp:720-735). tris = nTriangles x 36 f32 exactly as
+ * Triangle_encoded (main.cpp:51-60); nodes = nNodes x 12 f32 exactly as
+ * BVHNode_encoded (main.cpp:69-73) including the dummy node 0, root at 1. */
+int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTriangles, const float* nodes, int nNodes);
+
+/* Upload the HDR environment (replaces hdrMap/hdrCache textures,
+ * ImportanceSampling_LowDiscrepancySequence/main.cpp:843-853). hdr = w x h x 3
+ * f32, row 0 = first scanline; cache = calculateHdrCache output (nullable: the
+ * library computes it). hdrResolution := w. hdr == NULL clears the env (black). */
+int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache);
+
+/* PT_BASIC_CPU_COMPAT shape list: n x 24 f32 records (layout in pt_scene.h). */
+int pt_upload_shapes(pt_ctx* ctx, const float* shapes, int n);
+
+/* One display() (OpenglRayTracing/main.cpp:558-603): 1 spp per owned pixel and
+ * the running-mean update of the device-resident accumulation (pass1.fsh:868-871);
+ * frameCounter = 0 resets the mean (mix weight 1). eye[3]; cameraRotate[16]
+ * column-major = inverse(lookAt(eye, 0, up)) (main.cpp:570-573). accum_rgba
+ * (nullable) receives width x height x 4 f32 after the frame. For
+ * PT_BASIC_CPU_COMPAT frameCounter is the sample index k and accum is the sum
+ * buffer `image` (BasicRayTracingWithC++/main.cpp:356-431). */
+int pt_render_frame(pt_ctx* ctx, const float eye[3], const float cameraRotate[16],
+                    uint32_t frameCounter, float* accum_rgba);
+/* Same without synchronising or downloading. */
+int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16],
+                          uint32_t frameCounter);
+
+/* Batch hitBVH (pass1.fsh:335-382; BVH/main.cpp:571 debug-ray query). rays =
+ * n x 6 f32 (origin, direction); miss -> t = 2147483648.f, tri = -1. */
+int pt_trace_closest(pt_ctx* ctx, const float* rays, int n, float* t_out, int* tri_out);
+
+/* Accumulation buffer access (lastFrame texture, main.cpp:763-764). */
+int pt_download_accum(pt_ctx* ctx, float* accum_rgba);
+int pt_upload_accum(pt_ctx* ctx, const float* accum_rgba);
+int pt_clear_accum(pt_ctx* ctx);
+int pt_accum_device_ptr(pt_ctx* ctx, void** dptr); /* width*height*4 f32, device memory */
+
+/* pass3.fsh tonemap c / (1 + (0.3r+0.6g+0.1b)/limit) of the accumulation,
+ * optional gamma (pass3.fsh:14-24 keeps it commented out: gamma <= 0). rgb_out
+ * = width x height x 3 f32 host buffer. */
+int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out);
+
+/* Multi-GPU tile exchange: pack this rank's owned pixels into a contiguous
+ * device buffer (count = pt_owned_pixel_count), and unpack another rank's
+ * packed pixels into this context's accumulation. Pointers are device memory;
+ * the caller moves the packed buffers (RCCL gather over xGMI). */
+int pt_owned_pixel_count(pt_ctx* ctx, int rank, int world, int64_t* count);
+int pt_pack_owned(pt_ctx* ctx, void* dpacked);
+int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked);
+
+/* Stream interop: render on the caller's HIP stream (e.g. torch's current
+ * stream). NULL restores the context's own stream. */
+int pt_set_stream(pt_ctx* ctx, void* hip_stream);
+int pt_synchronize(pt_ctx* ctx);
+int pt_get_stats(pt_ctx* ctx, pt_frame_stats* stats);   /* synchronises the stream */
+int pt_reset_stats(pt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_ABI_H */

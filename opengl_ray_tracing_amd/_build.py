@@ -1,0 +1,94 @@
+"""In-tree native build: libpt.so (HIP kernels + C-ABI runtime + host scene
+prep) for gfx950, and the test-only oracle (oracle/liboracle.so).
+
+The built shared objects stay in the source tree (git-ignored) so they travel
+to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+INCLUDE = ROOT / "include"
+BUILD = PKG / "_objs"
+LIB = PKG / "libpt.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "liboracle.so"
+
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = "gfx950"
+
+HIP_FLAGS = [
+    f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+    # exact single-rounding float semantics, matching the CPU checker
+    "-ffp-contract=off",
+    "-Wall", "-Wno-unused-function",
+]
+CXX_FLAGS = ["-O2", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+             "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"]
+
+SOURCES = {
+    "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h"]),
+    "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h"]),
+    "scene.o": ("cxx", CSRC / "scene.cpp", [INCLUDE / "pt_scene.h"]),
+}
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed: " + " ".join(map(str, cmd)) + "\n" + r.stdout + r.stderr)
+    return r
+
+
+def build_native(force: bool = False, verbose: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    jobs = []
+    objs = []
+    for obj, (kind, src, deps) in SOURCES.items():
+        out = BUILD / obj
+        objs.append(out)
+        if force or _stale(out, [src, *deps]):
+            inc = [f"-I{INCLUDE}", f"-I{CSRC}"]
+            if kind == "hip":
+                cmd = [HIPCC, *HIP_FLAGS, *inc, "-c", str(src), "-o", str(out)]
+            else:
+                cmd = ["g++", *CXX_FLAGS, *inc, "-c", str(src), "-o", str(out)]
+            jobs.append(cmd)
+    if jobs:
+        with ThreadPoolExecutor(max_workers=min(4, len(jobs))) as ex:
+            for r in ex.map(_run, jobs):
+                if verbose and (r.stdout or r.stderr):
+                    sys.stderr.write(r.stdout + r.stderr)
+    if force or jobs or _stale(LIB, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)])
+    return LIB
+
+
+def build_oracle(force: bool = False) -> Path:
+    """Test infrastructure only (see oracle/pt_oracle.h)."""
+    src = [ORACLE_DIR / "pt_oracle.c", ORACLE_DIR / "pt_oracle.h"]
+    if force or _stale(ORACLE_LIB, src):
+        _run(["make", "-s", "-C", str(ORACLE_DIR), "-B" if force else "all"])
+    return ORACLE_LIB
+
+
+if __name__ == "__main__":
+    build_native(force="--force" in sys.argv, verbose=True)
+    build_oracle(force="--force" in sys.argv)
+    print(LIB)
+    print(ORACLE_LIB)

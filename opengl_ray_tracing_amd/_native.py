@@ -1,0 +1,123 @@
+"""ctypes binding of libpt.so (include/pt_abi.h + include/pt_scene.h).
+
+The product path has no fallback: if libpt.so is missing or fails to load,
+every entry point raises. Build it with ``python -m opengl_ray_tracing_amd._build``
+or ``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+from . import _build
+
+_lib = None
+
+c_float_p = C.POINTER(C.c_float)
+c_int_p = C.POINTER(C.c_int)
+
+
+class PtConfig(C.Structure):
+    _fields_ = [
+        ("width", C.c_int), ("height", C.c_int), ("integrator", C.c_int), ("max_bounce", C.c_int),
+        ("device_id", C.c_int), ("tile_rank", C.c_int), ("tile_world", C.c_int), ("tile_size", C.c_int),
+        ("flags", C.c_uint32), ("basic_samples", C.c_int), ("basic_seed", C.c_uint32),
+    ]
+
+
+class PtFrameStats(C.Structure):
+    _fields_ = [
+        ("rays", C.c_uint64), ("node_fetch", C.c_uint64), ("tri_fetch", C.c_uint64),
+        ("mat_fetch", C.c_uint64), ("tex_fetch", C.c_uint64), ("kernel_ms", C.c_float),
+        ("kernel_ms_total", C.c_float), ("launches", C.c_int), ("max_stack", C.c_int),
+    ]
+
+
+class PtMaterial(C.Structure):
+    _fields_ = [
+        ("emissive", C.c_float * 3), ("baseColor", C.c_float * 3),
+        ("subsurface", C.c_float), ("metallic", C.c_float), ("specular", C.c_float),
+        ("specularTint", C.c_float), ("roughness", C.c_float), ("anisotropic", C.c_float),
+        ("sheen", C.c_float), ("sheenTint", C.c_float), ("clearcoat", C.c_float),
+        ("clearcoatGloss", C.c_float), ("IOR", C.c_float), ("transmission", C.c_float),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in include/pt_abi.h and include/pt_scene.h
+SIGNATURES = {
+    # pt_abi.h
+    "pt_device_count": (C.c_int, [c_int_p]),
+    "pt_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(PtConfig)]),
+    "pt_destroy": (None, [C.c_void_p]),
+    "pt_last_error": (C.c_char_p, [C.c_void_p]),
+    "pt_upload_scene": (C.c_int, [C.c_void_p, c_float_p, C.c_int, c_float_p, C.c_int]),
+    "pt_upload_env": (C.c_int, [C.c_void_p, c_float_p, C.c_int, C.c_int, c_float_p]),
+    "pt_upload_shapes": (C.c_int, [C.c_void_p, c_float_p, C.c_int]),
+    "pt_render_frame": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32, c_float_p]),
+    "pt_render_frame_async": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32]),
+    "pt_trace_closest": (C.c_int, [C.c_void_p, c_float_p, C.c_int, c_float_p, c_int_p]),
+    "pt_download_accum": (C.c_int, [C.c_void_p, c_float_p]),
+    "pt_upload_accum": (C.c_int, [C.c_void_p, c_float_p]),
+    "pt_clear_accum": (C.c_int, [C.c_void_p]),
+    "pt_accum_device_ptr": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "pt_tonemap": (C.c_int, [C.c_void_p, C.c_float, C.c_float, c_float_p]),
+    "pt_owned_pixel_count": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int64)]),
+    "pt_pack_owned": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pt_unpack_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "pt_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pt_synchronize": (C.c_int, [C.c_void_p]),
+    "pt_get_stats": (C.c_int, [C.c_void_p, C.POINTER(PtFrameStats)]),
+    "pt_reset_stats": (C.c_int, [C.c_void_p]),
+    # pt_scene.h
+    "pt_material_default": (None, [C.POINTER(PtMaterial)]),
+    "pt_scene_create": (C.c_int, [C.POINTER(C.c_void_p)]),
+    "pt_scene_destroy": (None, [C.c_void_p]),
+    "pt_scene_read_obj": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(PtMaterial), c_float_p, C.c_int]),
+    "pt_scene_read_obj_text": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(PtMaterial), c_float_p, C.c_int]),
+    "pt_scene_add_mesh": (C.c_int, [C.c_void_p, c_float_p, C.c_int, c_int_p, C.c_int, C.POINTER(PtMaterial),
+                                    c_float_p, C.c_int]),
+    "pt_scene_num_triangles": (C.c_int, [C.c_void_p]),
+    "pt_scene_build_bvh": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "pt_scene_num_nodes": (C.c_int, [C.c_void_p]),
+    "pt_scene_depth": (C.c_int, [C.c_void_p]),
+    "pt_scene_encode": (C.c_int, [C.c_void_p, c_float_p, c_float_p]),
+    "pt_transform_matrix": (None, [c_float_p, c_float_p, c_float_p, c_float_p]),
+    "pt_orbit_camera": (None, [C.c_float, C.c_float, C.c_float, c_float_p, c_float_p]),
+    "pt_hdr_load": (C.c_int, [C.c_char_p, c_int_p, c_int_p, C.POINTER(c_float_p)]),
+    "pt_hdr_decode": (C.c_int, [C.c_void_p, C.c_int64, c_int_p, c_int_p, C.POINTER(c_float_p)]),
+    "pt_free": (None, [C.c_void_p]),
+    "pt_hdr_cache": (C.c_int, [c_float_p, C.c_int, C.c_int, c_float_p]),
+}
+
+
+def lib_path() -> Path:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = False):
+    """Load libpt.so (raises if absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not path.exists():
+        if not build_if_missing:
+            raise RuntimeError(f"native library {path} is missing; run opengl_ray_tracing_amd._build.build_native()")
+        _build.build_native()
+    lib = C.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class PtError(RuntimeError):
+    pass
+
+
+def check(rc: int, ctx=None, what: str = ""):
+    if rc != 0:
+        msg = load().pt_last_error(ctx)
+        raise PtError(f"{what} failed with {rc}: {msg.decode() if msg else ''}")

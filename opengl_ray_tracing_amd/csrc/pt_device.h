@@ -1,0 +1,381 @@
+// pt_device.h -- device-side math, RNG, environment and BRDF for the MI355X
+// path tracer. Every function restates one routine of the reference's
+// pass1.fsh (cited), in the same float evaluation order as oracle/pt_oracle.c
+// so the GPU and the CPU checker round identically wherever the hardware
+// operations are correctly rounded (+,-,*,/,sqrt; the build uses
+// -ffp-contract=off and IEEE fp32 division/sqrt). Transcendentals come from
+// ROCm's ocml and may differ by an ulp from glibc: parity is stated with a
+// tolerance for them.
+//
+// IS = ImportanceSampling_LowDiscrepancySequence/shaders/pass1.fsh,
+// D = DisneyBRDF/shaders/pass1.fsh, O = OpenglRayTracing/shaders/pass1.fsh.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_kernels.h"
+
+#define PT_PI 3.1415926f          // IS:23
+#define PT_INF 2147483647.0f      // IS:24 (2^31 in f32)
+
+namespace pt {
+
+struct V3 {
+  float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 operator/(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return v3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+__device__ __forceinline__ V3 normalize(V3 v) {
+  float inv = 1.0f / sqrtf(dot(v, v));
+  return v * inv;
+}
+__device__ __forceinline__ float mixf(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+__device__ __forceinline__ V3 mixv(V3 x, V3 y, float a) {
+  return v3(mixf(x.x, y.x, a), mixf(x.y, y.y, a), mixf(x.z, y.z, a));
+}
+__device__ __forceinline__ float sqr(float x) { return x * x; }
+__device__ __forceinline__ V3 reflect3(V3 I, V3 N) {
+  float k = 2.0f * dot(N, I);
+  return I - N * k;
+}
+__device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
+
+// ------------------------------------------------------------------ RNG
+// wang_hash IS:78-85
+__device__ __forceinline__ uint32_t wang(uint32_t& s) {
+  uint32_t x = s;
+  x = (x ^ 61u) ^ (x >> 16);
+  x *= 9u;
+  x = x ^ (x >> 4);
+  x *= 0x27d4eb2du;
+  x = x ^ (x >> 15);
+  s = x;
+  return x;
+}
+// rand IS:87-89
+__device__ __forceinline__ float randf(uint32_t& s) { return (float)wang(s) / 4294967296.0f; }
+
+// Sobol direction numbers IS:92-94 (8 dims x 32), in constant memory.
+extern __constant__ uint32_t kSobolV[8 * 32];
+
+// sobol IS:101-109 with the documented dims >= 8 extension (oracle: sobol_bits)
+__device__ __forceinline__ float sobolf(uint32_t d, uint32_t i) {
+  uint32_t result = 0;
+  const uint32_t* V = kSobolV + (d & 7u) * 32u;
+  for (uint32_t j = 0; i != 0; i >>= 1, j++)
+    if ((i & 1u) != 0) result ^= V[j];
+  if (d >= 8u) {
+    uint32_t h = d;
+    result ^= wang(h);
+  }
+  return (float)result * (1.0f / (float)0xFFFFFFFFu);
+}
+__device__ __forceinline__ uint32_t grayCode(uint32_t i) { return i ^ (i >> 1); }
+
+// CranleyPattersonRotation IS:118-136
+__device__ __forceinline__ void cranleyPatterson(int px, int py, float& u_, float& v_) {
+  uint32_t pseed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + 59u * 26699u) | 1u;
+  float u = (float)wang(pseed) / 4294967296.0f;
+  float v = (float)wang(pseed) / 4294967296.0f;
+  float x = u_ + u;
+  if (x > 1.0f) x -= 1.0f;
+  if (x < 0.0f) x += 1.0f;
+  float y = v_ + v;
+  if (y > 1.0f) y -= 1.0f;
+  if (y < 0.0f) y += 1.0f;
+  u_ = x;
+  v_ = y;
+}
+
+// ------------------------------------------------------------ material
+struct Material {  // IS:41-56
+  V3 emissive, baseColor;
+  float subsurface, metallic, specular, specularTint, roughness, anisotropic;
+  float sheen, sheenTint, clearcoat, clearcoatGloss;
+};
+// getMaterial IS:207-232 from the 36-float Triangle_encoded record
+__device__ __forceinline__ Material loadMaterial(const float* rec) {
+  const float4* q = reinterpret_cast<const float4*>(rec + 16);  // floats 16..35 (records are 144 B, 16 B aligned)
+  float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+  // floats: 16 17 18 | 19 20 21 | 22 23 24 | 25 26 27 | 28 29 30 | 31 32 33 | 34 35
+  // emissive = 18,19,20; baseColor = 21,22,23; param1 = 24..26; param2 = 27..29; param3 = 30..32; param4 = 33..35
+  Material m;
+  m.emissive = v3(a.z, a.w, b.x);
+  m.baseColor = v3(b.y, b.z, b.w);
+  m.subsurface = c.x; m.metallic = c.y; m.specular = c.z;
+  m.specularTint = c.w; m.roughness = d.x; m.anisotropic = d.y;
+  m.sheen = d.z; m.sheenTint = d.w; m.clearcoat = e.x;
+  m.clearcoatGloss = e.y;
+  return m;
+}
+
+// ------------------------------------------------------------ environment
+__device__ __forceinline__ float4 texNearest(const float4* img, int w, int h, float u, float v) {
+  float fx = floorf(u * (float)w);
+  float fy = floorf(v * (float)h);
+  fx = fminf(fmaxf(fx, 0.0f), (float)(w - 1));
+  fy = fminf(fmaxf(fy, 0.0f), (float)(h - 1));
+  int x = (int)fx, y = (int)fy;
+  return img[y * w + x];
+}
+// SampleSphericalMap IS:175-181 / toSphericalCoord IS:638-644
+__device__ __forceinline__ void toSpherical(V3 v, float& u, float& w) {
+  float a = atan2f(v.z, v.x), b = asinf(v.y);
+  a = a / (2.0f * PT_PI);
+  b = b / PT_PI;
+  a = a + 0.5f;
+  b = b + 0.5f;
+  u = a;
+  w = 1.0f - b;
+}
+// sampleHdr IS:184-189 (clamped at 10)
+__device__ __forceinline__ V3 sampleHdr(const Env& e, V3 v) {
+  if (!e.hdr) return v3(0, 0, 0);
+  float u, w;
+  toSpherical(normalize(v), u, w);
+  float4 c = texNearest(e.hdr, e.w, e.h, u, w);
+  return v3(fminf(c.x, 10.0f), fminf(c.y, 10.0f), fminf(c.z, 10.0f));
+}
+// hdrColor IS:647-651 (unclamped)
+__device__ __forceinline__ V3 hdrColor(const Env& e, V3 L) {
+  if (!e.hdr) return v3(0, 0, 0);
+  float u, w;
+  toSpherical(normalize(L), u, w);
+  float4 c = texNearest(e.hdr, e.w, e.h, u, w);
+  return v3(c.x, c.y, c.z);
+}
+// SampleHdr IS:573-585
+__device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
+  float x = 0.0f, y = 0.0f;
+  if (e.cache) {
+    float4 c = texNearest(e.cache, e.w, e.h, xi1, xi2);
+    x = c.x;
+    y = c.y;
+  }
+  y = 1.0f - y;
+  float phi = 2.0f * PT_PI * (x - 0.5f);
+  float theta = PT_PI * (y - 0.5f);
+  return v3(cosf(theta) * cosf(phi), sinf(theta), cosf(theta) * sinf(phi));
+}
+// hdrPdf IS:655-666 (sin of the elevation: reference quirk kept)
+__device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
+  float u, w;
+  toSpherical(normalize(L), u, w);
+  float pdf = e.cache ? texNearest(e.cache, e.w, e.h, u, w).z : 0.0f;
+  float theta = PT_PI * (0.5f - w);
+  float sin_theta = fmaxf(sinf(theta), 1e-10f);
+  float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
+  return pdf * p_convert;
+}
+
+// ------------------------------------------------------------ BRDF IS:386-711
+__device__ __forceinline__ float SchlickFresnel(float u) {
+  float m = fminf(fmaxf(1.0f - u, 0.0f), 1.0f);
+  float m2 = m * m;
+  return m2 * m2 * m;
+}
+__device__ __forceinline__ float GTR1(float NdotH, float a) {
+  if (a >= 1.0f) return 1.0f / PT_PI;
+  float a2 = a * a;
+  float t = 1.0f + (a2 - 1.0f) * NdotH * NdotH;
+  return (a2 - 1.0f) / (PT_PI * logf(a2) * t);
+}
+__device__ __forceinline__ float GTR2(float NdotH, float a) {
+  float a2 = a * a;
+  float t = 1.0f + (a2 - 1.0f) * NdotH * NdotH;
+  return a2 / (PT_PI * t * t);
+}
+__device__ __forceinline__ float GTR2_aniso(float NdotH, float HdotX, float HdotY, float ax, float ay) {
+  return 1.0f / (PT_PI * ax * ay * sqr(sqr(HdotX / ax) + sqr(HdotY / ay) + NdotH * NdotH));
+}
+__device__ __forceinline__ float smithG_GGX(float NdotV, float alphaG) {
+  float a = alphaG * alphaG;
+  float b = NdotV * NdotV;
+  return 1.0f / (NdotV + sqrtf(a + b - a * b));
+}
+__device__ __forceinline__ float smithG_GGX_aniso(float NdotV, float VdotX, float VdotY, float ax, float ay) {
+  return 1.0f / (NdotV + sqrtf(sqr(VdotX * ax) + sqr(VdotY * ay) + sqr(NdotV)));
+}
+struct Tints {
+  V3 Cdlin, Cspec0, Csheen;
+};
+__device__ __forceinline__ Tints tints(const Material& m) {
+  Tints t;
+  V3 Cdlin = m.baseColor;
+  float Cdlum = 0.3f * Cdlin.x + 0.6f * Cdlin.y + 0.1f * Cdlin.z;
+  V3 Ctint = (Cdlum > 0.0f) ? Cdlin / Cdlum : v3(1, 1, 1);
+  V3 Cspec = mixv(v3(1, 1, 1), Ctint, m.specularTint) * m.specular;
+  t.Cdlin = Cdlin;
+  t.Cspec0 = mixv(Cspec * 0.08f, Cdlin, m.metallic);
+  t.Csheen = mixv(v3(1, 1, 1), Ctint, m.sheenTint);
+  return t;
+}
+// BRDF_Evaluate_aniso IS:423-482 == D:381-440
+__device__ __forceinline__ V3 brdfAniso(V3 V, V3 N, V3 L, V3 X, V3 Y, const Material& m) {
+  float NdotL = dot(N, L);
+  float NdotV = dot(N, V);
+  if (NdotL < 0 || NdotV < 0) return v3(0, 0, 0);
+  V3 H = normalize(L + V);
+  float NdotH = dot(N, H);
+  float LdotH = dot(L, H);
+  Tints tt = tints(m);
+  float Fd90 = 0.5f + 2.0f * LdotH * LdotH * m.roughness;
+  float FL = SchlickFresnel(NdotL);
+  float FV = SchlickFresnel(NdotV);
+  float Fd = mixf(1.0f, Fd90, FL) * mixf(1.0f, Fd90, FV);
+  float Fss90 = LdotH * LdotH * m.roughness;
+  float Fss = mixf(1.0f, Fss90, FL) * mixf(1.0f, Fss90, FV);
+  float ss = 1.25f * (Fss * (1.0f / (NdotL + NdotV) - 0.5f) + 0.5f);
+  float aspect = sqrtf(1.0f - m.anisotropic * 0.9f);
+  float ax = fmaxf(0.001f, sqr(m.roughness) / aspect);
+  float ay = fmaxf(0.001f, sqr(m.roughness) * aspect);
+  float Ds = GTR2_aniso(NdotH, dot(H, X), dot(H, Y), ax, ay);
+  float FH = SchlickFresnel(LdotH);
+  V3 Fs = mixv(tt.Cspec0, v3(1, 1, 1), FH);
+  float Gs = smithG_GGX_aniso(NdotL, dot(L, X), dot(L, Y), ax, ay);
+  Gs *= smithG_GGX_aniso(NdotV, dot(V, X), dot(V, Y), ax, ay);
+  V3 specular = (Fs * Gs) * Ds;
+  float Dr = GTR1(NdotH, mixf(0.1f, 0.001f, m.clearcoatGloss));
+  float Fr = mixf(0.04f, 1.0f, FH);
+  float Gr = smithG_GGX(NdotL, 0.25f) * smithG_GGX(NdotV, 0.25f);
+  float cc = 0.25f * Gr * Fr * Dr * m.clearcoat;
+  V3 Fsheen = tt.Csheen * (FH * m.sheen);
+  float kd = (1.0f / PT_PI) * mixf(Fd, ss, m.subsurface);
+  V3 diffuse = tt.Cdlin * kd + Fsheen;
+  V3 r = diffuse * (1.0f - m.metallic) + specular;
+  return r + v3(cc, cc, cc);
+}
+// BRDF_Evaluate IS:587-636
+__device__ __forceinline__ V3 brdfIso(V3 V, V3 N, V3 L, const Material& m) {
+  float NdotL = dot(N, L);
+  float NdotV = dot(N, V);
+  if (NdotL < 0 || NdotV < 0) return v3(0, 0, 0);
+  V3 H = normalize(L + V);
+  float NdotH = dot(N, H);
+  float LdotH = dot(L, H);
+  Tints tt = tints(m);
+  float Fd90 = 0.5f + 2.0f * LdotH * LdotH * m.roughness;
+  float FL = SchlickFresnel(NdotL);
+  float FV = SchlickFresnel(NdotV);
+  float Fd = mixf(1.0f, Fd90, FL) * mixf(1.0f, Fd90, FV);
+  float Fss90 = LdotH * LdotH * m.roughness;
+  float Fss = mixf(1.0f, Fss90, FL) * mixf(1.0f, Fss90, FV);
+  float ss = 1.25f * (Fss * (1.0f / (NdotL + NdotV) - 0.5f) + 0.5f);
+  float alpha = fmaxf(0.001f, sqr(m.roughness));
+  float Ds = GTR2(NdotH, alpha);
+  float FH = SchlickFresnel(LdotH);
+  V3 Fs = mixv(tt.Cspec0, v3(1, 1, 1), FH);
+  float Gs = smithG_GGX(NdotL, m.roughness);
+  Gs *= smithG_GGX(NdotV, m.roughness);
+  float Dr = GTR1(NdotH, mixf(0.1f, 0.001f, m.clearcoatGloss));
+  float Fr = mixf(0.04f, 1.0f, FH);
+  float Gr = smithG_GGX(NdotL, 0.25f) * smithG_GGX(NdotV, 0.25f);
+  V3 Fsheen = tt.Csheen * (FH * m.sheen);
+  float kd = (1.0f / PT_PI) * mixf(Fd, ss, m.subsurface);
+  V3 diffuse = tt.Cdlin * kd + Fsheen;
+  V3 specular = (Fs * Gs) * Ds;
+  float cc = 0.25f * Gr * Fr * Dr * m.clearcoat;
+  V3 r = diffuse * (1.0f - m.metallic) + specular;
+  return r + v3(cc, cc, cc);
+}
+// BRDF_Pdf IS:669-706
+__device__ __forceinline__ float brdfPdf(V3 V, V3 N, V3 L, const Material& m) {
+  float NdotL = dot(N, L);
+  float NdotV = dot(N, V);
+  if (NdotL < 0 || NdotV < 0) return 0.0f;
+  V3 H = normalize(L + V);
+  float NdotH = dot(N, H);
+  float LdotH = dot(L, H);
+  float alpha = fmaxf(0.001f, sqr(m.roughness));
+  float Ds = GTR2(NdotH, alpha);
+  float Dr = GTR1(NdotH, mixf(0.1f, 0.001f, m.clearcoatGloss));
+  float pdf_diffuse = NdotL / PT_PI;
+  float pdf_specular = Ds * NdotH / (4.0f * LdotH);
+  float pdf_clearcoat = Dr * NdotH / (4.0f * LdotH);
+  float r_diffuse = 1.0f - m.metallic;
+  float r_specular = 1.0f;
+  float r_clearcoat = 0.25f * m.clearcoat;
+  float r_sum = r_diffuse + r_specular + r_clearcoat;
+  float p_diffuse = r_diffuse / r_sum;
+  float p_specular = r_specular / r_sum;
+  float p_clearcoat = r_clearcoat / r_sum;
+  float pdf = p_diffuse * pdf_diffuse + p_specular * pdf_specular + p_clearcoat * pdf_clearcoat;
+  return fmaxf(1e-10f, pdf);
+}
+__device__ __forceinline__ float misWeight(float a, float b) {  // IS:708-711
+  float t = a * a;
+  return t / (b * b + t);
+}
+// toNormalHemisphere IS:153-159
+__device__ __forceinline__ V3 toNormalHemisphere(V3 v, V3 N) {
+  V3 helper = v3(1, 0, 0);
+  if (fabsf(N.x) > 0.999f) helper = v3(0, 0, 1);
+  V3 tangent = normalize(cross(N, helper));
+  V3 bitangent = normalize(cross(N, tangent));
+  return (tangent * v.x + bitangent * v.y) + N * v.z;
+}
+// getTangent IS:161-172 (swapped naming kept)
+__device__ __forceinline__ void getTangent(V3 N, V3& tangent, V3& bitangent) {
+  V3 helper = v3(1, 0, 0);
+  if (fabsf(N.x) > 0.999f) helper = v3(0, 0, 1);
+  bitangent = normalize(cross(N, helper));
+  tangent = normalize(cross(N, bitangent));
+}
+// SampleHemisphere D:90-95
+__device__ __forceinline__ V3 sampleHemisphereRand(uint32_t& seed) {
+  float z = randf(seed);
+  float r = fmaxf(0.0f, sqrtf(1.0f - z * z));
+  float phi = 2.0f * PT_PI * randf(seed);
+  return v3(r * cosf(phi), r * sinf(phi), z);
+}
+// SampleCosineHemisphere IS:485-496
+__device__ __forceinline__ V3 sampleCosine(float xi_1, float xi_2, V3 N) {
+  float r = sqrtf(xi_1);
+  float theta = xi_2 * 2.0f * PT_PI;
+  float x = r * cosf(theta);
+  float y = r * sinf(theta);
+  float z = sqrtf(1.0f - x * x - y * y);
+  return toNormalHemisphere(v3(x, y, z), N);
+}
+// SampleGTR2 IS:499-516 / SampleGTR1 IS:519-536
+__device__ __forceinline__ V3 sampleGTR(float xi_1, float xi_2, V3 V, V3 N, float alpha, bool gtr1) {
+  float phi_h = 2.0f * PT_PI * xi_1;
+  float sin_phi_h = sinf(phi_h);
+  float cos_phi_h = cosf(phi_h);
+  float cos_theta_h;
+  if (gtr1)
+    cos_theta_h = sqrtf((1.0f - powf(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));
+  else
+    cos_theta_h = sqrtf((1.0f - xi_2) / (1.0f + (alpha * alpha - 1.0f) * xi_2));
+  float sin_theta_h = sqrtf(fmaxf(0.0f, 1.0f - cos_theta_h * cos_theta_h));
+  V3 H = v3(sin_theta_h * cos_phi_h, sin_theta_h * sin_phi_h, cos_theta_h);
+  H = toNormalHemisphere(H, N);
+  return reflect3(-V, H);
+}
+// SampleBRDF IS:539-570
+__device__ __forceinline__ V3 sampleBRDF(float xi_1, float xi_2, float xi_3, V3 V, V3 N, const Material& m) {
+  float alpha_GTR1 = mixf(0.1f, 0.001f, m.clearcoatGloss);
+  float alpha_GTR2 = fmaxf(0.001f, sqr(m.roughness));
+  float r_diffuse = 1.0f - m.metallic;
+  float r_specular = 1.0f;
+  float r_clearcoat = 0.25f * m.clearcoat;
+  float r_sum = r_diffuse + r_specular + r_clearcoat;
+  float p_diffuse = r_diffuse / r_sum;
+  float p_specular = r_specular / r_sum;
+  float rd = xi_3;
+  if (rd <= p_diffuse) return sampleCosine(xi_1, xi_2, N);
+  if (p_diffuse < rd && rd <= p_diffuse + p_specular) return sampleGTR(xi_1, xi_2, V, N, alpha_GTR2, false);
+  if (p_diffuse + p_specular < rd) return sampleGTR(xi_1, xi_2, V, N, alpha_GTR1, true);
+  return v3(0, 1, 0);
+}
+
+}  // namespace pt

@@ -1,0 +1,88 @@
+// pt_kernels.h -- kernel parameter blocks and launchers shared by
+// pt_kernels.hip (device) and pt_runtime.cpp (host).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pt {
+
+constexpr int BLOCK = 256;        // 4 waves of 64
+constexpr int LDS_STACK = 32;     // traversal stack entries per lane kept in LDS (32 KiB per block)
+constexpr int NUM_QUEUES = 8;     // work counters, one per blockIdx % 8 group (XCD round-robin)
+constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
+constexpr int REF_NONE = (int)0x80000000;
+constexpr int MAX_LEAF = 1 << LEAF_CNT_BITS;
+constexpr int MAX_TRIS = (1 << (31 - LEAF_CNT_BITS)) - 1;
+
+// Device-resident scene (relaid out at upload, see pt_runtime.cpp)
+struct SceneView {
+  const float4* geo;   // 4 float4 per triangle: (p1, w=dot(Ng,p1)), (p2, 0), (p3, 0), (Ng, 0)
+  const float* attr;   // 36 f32 per triangle: the Triangle_encoded record (normals, material)
+  const float4* bvh;   // 4 float4 per reference node id: (L.AA, Lref) (L.BB, Rref) (R.AA, -) (R.BB, -)
+  int rootRef;         // encoded reference to node 1
+  int nTri;
+};
+
+// HDR environment (hdrMap + hdrCache textures, IS main.cpp:843-853), float4 texels
+struct Env {
+  const float4* hdr;    // w x h, rgb in xyz (row 0 = first scanline); null = black
+  const float4* cache;  // calculateHdrCache: (x, y, pdf); null = none
+  int w, h, res;        // res = hdrResolution
+};
+
+struct RenderParams {
+  SceneView scene;
+  Env env;
+  int width, height;
+  uint32_t frameCounter;
+  int maxBounce;
+  float eye[3];
+  float cam[16];
+  float4* accum;
+  int* queue;           // NUM_QUEUES counters, zeroed before each launch
+  int perQueue;         // items per queue
+  int numItems;         // 8x8 wave tiles owned by this rank
+  int shardSize;        // shard tile edge (multiple of 8)
+  int shardTiles;       // (shardSize/8)^2
+  int shardsX;          // shard tiles per row
+  int rank, world;
+  int* ovf;             // traversal stack overflow (per thread ovfDepth ints), may be null
+  int ovfDepth;
+  unsigned long long* stats;  // [rays, nodes, tris, mats, texels]
+};
+
+struct TraceParams {
+  SceneView scene;
+  const float* rays;
+  int n;
+  float* t;
+  int* tri;
+  int* ovf;
+  int ovfDepth;
+};
+
+struct BasicParams {
+  const float* shapes;
+  int nShapes;
+  int width, height;
+  uint32_t sample, seed;
+  int maxDepth;
+  float brightness;
+  float4* accum;
+  unsigned long long* stats;
+};
+
+struct PackParams {
+  int width, height, shardSize, shardsX, rank, world;
+  long count;
+};
+
+hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count);
+hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, int* nb);
+hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
+hipError_t launchBasic(const BasicParams& p, hipStream_t s);
+hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s);
+hipError_t launchPack(const PackParams& p, const float4* accum, float4* packed, hipStream_t s);
+hipError_t launchUnpack(const PackParams& p, float4* accum, const float4* packed, hipStream_t s);
+
+}  // namespace pt

@@ -1,0 +1,591 @@
+// pt_runtime.cpp -- host implementation of the C-ABI in include/pt_abi.h:
+// device selection, scene/env upload with the MI355X re-layout, frame
+// launches, batch queries, accumulation access and multi-GPU tile pack.
+//
+// Compiled with -ffp-contract=off so the per-triangle unit normal and plane
+// offset precomputed here round exactly like the reference computes them
+// inline (pass1.fsh:263, :273).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pt_abi.h"
+#include "pt_kernels.h"
+#include "pt_scene.h"
+
+using namespace pt;
+
+struct pt_ctx {
+  pt_config cfg{};
+  std::string err;
+  hipStream_t own = nullptr, stream = nullptr;
+  std::vector<hipEvent_t> evs;  // begin/end pairs of the launches since the last reset
+  int launches = 0;
+  int numCU = 0;
+  // scene
+  float4* d_geo = nullptr;
+  float* d_attr = nullptr;
+  float4* d_bvh = nullptr;
+  int rootRef = REF_NONE;
+  int nTri = 0, nNodes = 0, depth = 0, maxStack = 0;
+  // env
+  float4* d_hdr = nullptr;
+  float4* d_cache = nullptr;
+  int hdrW = 0, hdrH = 0;
+  // BASIC shapes
+  float* d_shapes = nullptr;
+  int nShapes = 0;
+  // frame state
+  float4* d_accum = nullptr;
+  unsigned char* d_ctl = nullptr;  // [0,32) queue counters (zeroed per launch), [64,104) cumulative stats
+  int* d_ovf = nullptr;
+  size_t ovfInts = 0;
+  // shards
+  int shardSize = 32, shardsX = 0, shardsY = 0, numItems = 0, perQueue = 0;
+  // scratch for queries / tonemap / pack
+  float* d_rays = nullptr;
+  float* d_t = nullptr;
+  int* d_tri = nullptr;
+  size_t traceCap = 0;
+  float* d_rgb = nullptr;
+};
+
+static std::string g_create_err;
+
+#define CK(expr)                                                                     \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) {                                                          \
+      ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);                  \
+      return PT_E_HIP;                                                               \
+    }                                                                                \
+  } while (0)
+
+static int fail(pt_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+template <class T>
+static void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+extern "C" {
+
+int pt_device_count(int* n) {
+  if (!n) return PT_E_INVALID;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) c = 0;
+  *n = c;
+  return PT_OK;
+}
+
+const char* pt_last_error(pt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
+
+int pt_create(pt_ctx** out, const pt_config* cfg) {
+  if (!out || !cfg) return PT_E_INVALID;
+  *out = nullptr;
+  if (cfg->width <= 0 || cfg->height <= 0 || cfg->integrator < 0 || cfg->integrator > PT_BASIC_CPU_COMPAT ||
+      cfg->tile_world < 1 || cfg->tile_rank < 0 || cfg->tile_rank >= cfg->tile_world) {
+    g_create_err = "pt_create: invalid config";
+    return PT_E_INVALID;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    g_create_err = "pt_create: no HIP device";
+    return PT_E_NODEVICE;
+  }
+  if (cfg->device_id < 0 || cfg->device_id >= ndev) {
+    g_create_err = "pt_create: device_id out of range";
+    return PT_E_INVALID;
+  }
+  pt_ctx* ctx = new (std::nothrow) pt_ctx();
+  if (!ctx) return PT_E_NOMEM;
+  ctx->cfg = *cfg;
+  if (ctx->cfg.basic_samples <= 0) ctx->cfg.basic_samples = 128;
+  int ss = cfg->tile_size > 0 ? cfg->tile_size : 32;
+  if (ss % 8 != 0) {
+    delete ctx;
+    g_create_err = "pt_create: tile_size must be a multiple of 8";
+    return PT_E_INVALID;
+  }
+  ctx->shardSize = ss;
+  auto bail = [&](int code) {
+    g_create_err = ctx->err;
+    pt_destroy(ctx);
+    return code;
+  };
+#define CKC(expr)                                                     \
+  do {                                                                \
+    hipError_t e_ = (expr);                                           \
+    if (e_ != hipSuccess) {                                           \
+      ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);   \
+      return bail(PT_E_HIP);                                          \
+    }                                                                 \
+  } while (0)
+  CKC(hipSetDevice(cfg->device_id));
+  hipDeviceProp_t prop;
+  CKC(hipGetDeviceProperties(&prop, cfg->device_id));
+  ctx->numCU = prop.multiProcessorCount;
+  CKC(hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking));
+  ctx->stream = ctx->own;
+  const size_t npix = (size_t)cfg->width * cfg->height;
+  CKC(hipMalloc(&ctx->d_accum, npix * sizeof(float4)));
+  CKC(hipMemset(ctx->d_accum, 0, npix * sizeof(float4)));
+  CKC(hipMalloc(&ctx->d_ctl, 128));
+  CKC(hipMemset(ctx->d_ctl, 0, 128));
+  ctx->shardsX = (cfg->width + ss - 1) / ss;
+  ctx->shardsY = (cfg->height + ss - 1) / ss;
+  const int numShards = ctx->shardsX * ctx->shardsY;
+  const int owned = (numShards - cfg->tile_rank + cfg->tile_world - 1) / cfg->tile_world;
+  ctx->numItems = owned * (ss / 8) * (ss / 8);
+  ctx->perQueue = (ctx->numItems + NUM_QUEUES - 1) / NUM_QUEUES;
+#undef CKC
+  *out = ctx;
+  return PT_OK;
+}
+
+void pt_destroy(pt_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->cfg.device_id);
+  if (ctx->own) (void)hipStreamSynchronize(ctx->own);
+  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh);
+  dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
+  dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf);
+  dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
+  for (hipEvent_t e : ctx->evs) (void)hipEventDestroy(e);
+  if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+}
+
+// ------------------------------------------------------------ scene upload
+static inline void nrm3(const float* a, const float* b, const float* c, float N[3]) {
+  // normalize(cross(p2 - p1, p3 - p1)), glm order (oracle: hitTriangle)
+  float e1x = b[0] - a[0], e1y = b[1] - a[1], e1z = b[2] - a[2];
+  float e2x = c[0] - a[0], e2y = c[1] - a[1], e2z = c[2] - a[2];
+  float cx = e1y * e2z - e2y * e1z;
+  float cy = e1z * e2x - e2z * e1x;
+  float cz = e1x * e2y - e2x * e1y;
+  float inv = 1.0f / std::sqrt((cx * cx + cy * cy) + cz * cz);
+  N[0] = cx * inv; N[1] = cy * inv; N[2] = cz * inv;
+}
+
+int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes, int nNodes) {
+  if (!ctx || !tris || !nodes) return PT_E_INVALID;
+  if (nTri < 1 || nNodes < 2) return fail(ctx, PT_E_BADSCENE, "need >= 1 triangle and >= 2 nodes (dummy 0, root 1)");
+  if (nTri > MAX_TRIS) return fail(ctx, PT_E_BADSCENE, "too many triangles for the leaf encoding");
+  CK(hipSetDevice(ctx->cfg.device_id));
+  // geometry records
+  std::vector<float4> geo((size_t)nTri * 4);
+  for (int i = 0; i < nTri; i++) {
+    const float* t = tris + (size_t)i * 36;
+    float N[3];
+    nrm3(t, t + 3, t + 6, N);
+    float w = (N[0] * t[0] + N[1] * t[1]) + N[2] * t[2];
+    geo[4 * i + 0] = make_float4(t[0], t[1], t[2], w);
+    geo[4 * i + 1] = make_float4(t[3], t[4], t[5], 0.0f);
+    geo[4 * i + 2] = make_float4(t[6], t[7], t[8], 0.0f);
+    geo[4 * i + 3] = make_float4(N[0], N[1], N[2], 0.0f);
+  }
+  // node references (ivec3(texelFetch) truncation, pass1.fsh:238-243)
+  auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
+  std::string bad;
+  auto encodeRef = [&](int k) -> int {
+    if (k <= 0 || k >= nNodes) return REF_NONE;
+    int n = nodeN(k);
+    if (n > 0) {
+      int index = (int)nodes[(size_t)k * 12 + 4];
+      if (index < 0 || (long)index + n > nTri) { bad = "leaf range out of bounds at node " + std::to_string(k); return REF_NONE; }
+      if (n > MAX_LEAF) { bad = "leaf larger than 32 triangles at node " + std::to_string(k); return REF_NONE; }
+      return (int)~(((uint32_t)index << LEAF_CNT_BITS) | (uint32_t)(n - 1));
+    }
+    return k;
+  };
+  std::vector<float4> bvh((size_t)nNodes * 4, make_float4(0, 0, 0, 0));
+  const float inf = INFINITY;
+  for (int k = 1; k < nNodes; k++) {
+    if (nodeN(k) > 0) continue;
+    int L = (int)nodes[(size_t)k * 12 + 0], R = (int)nodes[(size_t)k * 12 + 1];
+    int lr = encodeRef(L), rr = encodeRef(R);
+    if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
+    float4 la = make_float4(inf, inf, inf, 0), lb = make_float4(-inf, -inf, -inf, 0);
+    float4 ra = la, rb = lb;
+    if (lr != REF_NONE) {
+      const float* c = nodes + (size_t)L * 12;
+      la = make_float4(c[6], c[7], c[8], 0); lb = make_float4(c[9], c[10], c[11], 0);
+    }
+    if (rr != REF_NONE) {
+      const float* c = nodes + (size_t)R * 12;
+      ra = make_float4(c[6], c[7], c[8], 0); rb = make_float4(c[9], c[10], c[11], 0);
+    }
+    int lrr = lr, rrr = rr;
+    std::memcpy(&la.w, &lrr, 4);
+    std::memcpy(&lb.w, &rrr, 4);
+    bvh[4 * (size_t)k + 0] = la; bvh[4 * (size_t)k + 1] = lb;
+    bvh[4 * (size_t)k + 2] = ra; bvh[4 * (size_t)k + 3] = rb;
+  }
+  int rootRef = encodeRef(1);
+  if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
+  // depth of the reachable tree (bounds the traversal stack)
+  int depth = 0;
+  {
+    std::vector<std::pair<int, int>> st{{1, 1}};
+    long visits = 0;
+    while (!st.empty()) {
+      auto [k, d] = st.back();
+      st.pop_back();
+      if (++visits > 2L * nNodes) return fail(ctx, PT_E_BADSCENE, "node graph is not a tree (cycle)");
+      depth = std::max(depth, d);
+      if (nodeN(k) > 0) continue;
+      int L = (int)nodes[(size_t)k * 12 + 0], R = (int)nodes[(size_t)k * 12 + 1];
+      if (L > 0 && L < nNodes) st.push_back({L, d + 1});
+      if (R > 0 && R < nNodes) st.push_back({R, d + 1});
+    }
+  }
+  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh);
+  CK(hipMalloc(&ctx->d_geo, geo.size() * sizeof(float4)));
+  CK(hipMalloc(&ctx->d_attr, (size_t)nTri * 36 * sizeof(float)));
+  CK(hipMalloc(&ctx->d_bvh, bvh.size() * sizeof(float4)));
+  CK(hipMemcpy(ctx->d_geo, geo.data(), geo.size() * sizeof(float4), hipMemcpyHostToDevice));
+  CK(hipMemcpy(ctx->d_attr, tris, (size_t)nTri * 36 * sizeof(float), hipMemcpyHostToDevice));
+  CK(hipMemcpy(ctx->d_bvh, bvh.data(), bvh.size() * sizeof(float4), hipMemcpyHostToDevice));
+  ctx->nTri = nTri;
+  ctx->nNodes = nNodes;
+  ctx->rootRef = rootRef;
+  ctx->depth = depth;
+  ctx->maxStack = depth + 1;
+  return PT_OK;
+}
+
+int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache) {
+  if (!ctx) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  dfree(ctx->d_hdr);
+  dfree(ctx->d_cache);
+  ctx->hdrW = ctx->hdrH = 0;
+  if (!hdr) return PT_OK;
+  if (w <= 0 || h <= 0) return PT_E_INVALID;
+  const size_t n = (size_t)w * h;
+  std::vector<float> own;
+  if (!cache) {
+    own.resize(n * 3);
+    if (pt_hdr_cache(hdr, w, h, own.data()) != 0) return fail(ctx, PT_E_INVALID, "hdr cache failed");
+    cache = own.data();
+  }
+  std::vector<float4> a(n), b(n);
+  for (size_t k = 0; k < n; k++) {
+    a[k] = make_float4(hdr[3 * k], hdr[3 * k + 1], hdr[3 * k + 2], 0.0f);
+    b[k] = make_float4(cache[3 * k], cache[3 * k + 1], cache[3 * k + 2], 0.0f);
+  }
+  CK(hipMalloc(&ctx->d_hdr, n * sizeof(float4)));
+  CK(hipMalloc(&ctx->d_cache, n * sizeof(float4)));
+  CK(hipMemcpy(ctx->d_hdr, a.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  CK(hipMemcpy(ctx->d_cache, b.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  ctx->hdrW = w;
+  ctx->hdrH = h;
+  return PT_OK;
+}
+
+int pt_upload_shapes(pt_ctx* ctx, const float* shapes, int n) {
+  if (!ctx || (!shapes && n > 0) || n < 0) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  dfree(ctx->d_shapes);
+  ctx->nShapes = 0;
+  if (n == 0) return PT_OK;
+  CK(hipMalloc(&ctx->d_shapes, (size_t)n * PT_SHAPE_FLOATS * sizeof(float)));
+  CK(hipMemcpy(ctx->d_shapes, shapes, (size_t)n * PT_SHAPE_FLOATS * sizeof(float), hipMemcpyHostToDevice));
+  ctx->nShapes = n;
+  return PT_OK;
+}
+
+static int defaultBounce(int integ) {
+  switch (integ) {
+    case PT_LAMBERT_O: return 2;           // O:385
+    case PT_DISNEY_UNIFORM_D: return 5;    // D:502
+    case PT_DISNEY_MIS_SOBOL_IS: return 2; // IS:861
+    default: return 8;                     // BasicRayTracingWithC++/main.cpp:254
+  }
+}
+
+// begin/end events of launch number ctx->launches (created on first use)
+static int launchEvents(pt_ctx* ctx, hipEvent_t* b, hipEvent_t* e) {
+  size_t need = 2 * (size_t)(ctx->launches + 1);
+  while (ctx->evs.size() < need) {
+    hipEvent_t ev;
+    CK(hipEventCreate(&ev));
+    ctx->evs.push_back(ev);
+  }
+  *b = ctx->evs[2 * ctx->launches];
+  *e = ctx->evs[2 * ctx->launches + 1];
+  return PT_OK;
+}
+
+static SceneView sceneView(const pt_ctx* ctx) {
+  SceneView s;
+  s.geo = ctx->d_geo;
+  s.attr = ctx->d_attr;
+  s.bvh = ctx->d_bvh;
+  s.rootRef = ctx->rootRef;
+  s.nTri = ctx->nTri;
+  return s;
+}
+
+// make sure the overflow stack covers `threads` threads
+static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth) {
+  *ovfDepth = ctx->maxStack > LDS_STACK ? ctx->maxStack - LDS_STACK + 1 : 0;
+  if (*ovfDepth == 0) return PT_OK;
+  size_t need = threads * (size_t)(*ovfDepth);
+  if (need > ctx->ovfInts) {
+    dfree(ctx->d_ovf);
+    CK(hipMalloc(&ctx->d_ovf, need * sizeof(int)));
+    ctx->ovfInts = need;
+  }
+  return PT_OK;
+}
+
+int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
+  if (!ctx) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  const pt_config& c = ctx->cfg;
+  unsigned long long* stats = reinterpret_cast<unsigned long long*>(ctx->d_ctl + 64);
+  CK(hipMemsetAsync(ctx->d_ctl, 0, 32, ctx->stream));
+  hipEvent_t evb, eve;
+  int erc = launchEvents(ctx, &evb, &eve);
+  if (erc) return erc;
+  if (c.integrator == PT_BASIC_CPU_COMPAT) {
+    if (!ctx->d_shapes) return fail(ctx, PT_E_NOSCENE, "no BASIC shapes uploaded");
+    BasicParams p;
+    p.shapes = ctx->d_shapes;
+    p.nShapes = ctx->nShapes;
+    p.width = c.width;
+    p.height = c.height;
+    p.sample = frameCounter;
+    p.seed = c.basic_seed;
+    p.maxDepth = c.max_bounce >= 0 ? c.max_bounce : 8;
+    p.brightness = (float)((double)(2.0f * 3.1415926f) * (1.0 / (double)c.basic_samples));
+    p.accum = ctx->d_accum;
+    p.stats = stats;
+    CK(hipEventRecord(evb, ctx->stream));
+    CK(launchBasic(p, ctx->stream));
+    CK(hipEventRecord(eve, ctx->stream));
+    ctx->launches++;
+    return PT_OK;
+  }
+  if (!ctx->d_bvh || !eye || !cameraRotate) return fail(ctx, ctx->d_bvh ? PT_E_INVALID : PT_E_NOSCENE, "no scene");
+  const bool count = (c.flags & PT_FLAG_COUNT_FETCHES) != 0;
+  const bool cull = !count && !(c.flags & PT_FLAG_NO_CULL);
+  int nb = 0;
+  CK(renderBlocksPerCU(c.integrator, cull, count, &nb));
+  if (nb < 1) nb = 1;
+  int grid = ctx->numCU * nb;
+  int ovfDepth = 0;
+  int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth);
+  if (rc) return rc;
+  RenderParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.scene = sceneView(ctx);
+  p.env.hdr = ctx->d_hdr;
+  p.env.cache = ctx->d_cache;
+  p.env.w = ctx->hdrW;
+  p.env.h = ctx->hdrH;
+  p.env.res = ctx->hdrW;
+  p.width = c.width;
+  p.height = c.height;
+  p.frameCounter = frameCounter;
+  p.maxBounce = c.max_bounce >= 0 ? c.max_bounce : defaultBounce(c.integrator);
+  std::memcpy(p.eye, eye, sizeof(p.eye));
+  std::memcpy(p.cam, cameraRotate, sizeof(p.cam));
+  p.accum = ctx->d_accum;
+  p.queue = reinterpret_cast<int*>(ctx->d_ctl);
+  p.perQueue = ctx->perQueue;
+  p.numItems = ctx->numItems;
+  p.shardSize = ctx->shardSize;
+  p.shardTiles = (ctx->shardSize / 8) * (ctx->shardSize / 8);
+  p.shardsX = ctx->shardsX;
+  p.rank = c.tile_rank;
+  p.world = c.tile_world;
+  p.ovf = ovfDepth ? ctx->d_ovf : nullptr;
+  p.ovfDepth = ovfDepth;
+  p.stats = stats;
+  CK(hipEventRecord(evb, ctx->stream));
+  CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
+  CK(hipEventRecord(eve, ctx->stream));
+  ctx->launches++;
+  return PT_OK;
+}
+
+int pt_render_frame(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter,
+                    float* accum_rgba) {
+  int rc = pt_render_frame_async(ctx, eye, cameraRotate, frameCounter);
+  if (rc) return rc;
+  if (accum_rgba) return pt_download_accum(ctx, accum_rgba);
+  return pt_synchronize(ctx);
+}
+
+int pt_trace_closest(pt_ctx* ctx, const float* rays, int n, float* t_out, int* tri_out) {
+  if (!ctx || n < 0 || (n > 0 && (!rays || !t_out || !tri_out))) return PT_E_INVALID;
+  if (!ctx->d_bvh) return fail(ctx, PT_E_NOSCENE, "no scene");
+  if (n == 0) return PT_OK;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  if ((size_t)n > ctx->traceCap) {
+    dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri);
+    CK(hipMalloc(&ctx->d_rays, (size_t)n * 6 * sizeof(float)));
+    CK(hipMalloc(&ctx->d_t, (size_t)n * sizeof(float)));
+    CK(hipMalloc(&ctx->d_tri, (size_t)n * sizeof(int)));
+    ctx->traceCap = n;
+  }
+  const bool cull = !(ctx->cfg.flags & (PT_FLAG_NO_CULL | PT_FLAG_COUNT_FETCHES));
+  int grid = (int)std::min<long>(((long)n + BLOCK - 1) / BLOCK, (long)ctx->numCU * 8);
+  int ovfDepth = 0;
+  int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(ctx->d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  TraceParams p;
+  p.scene = sceneView(ctx);
+  p.rays = ctx->d_rays;
+  p.n = n;
+  p.t = ctx->d_t;
+  p.tri = ctx->d_tri;
+  p.ovf = ovfDepth ? ctx->d_ovf : nullptr;
+  p.ovfDepth = ovfDepth;
+  CK(launchTrace(p, grid, ctx->stream, cull));
+  CK(hipMemcpyAsync(t_out, ctx->d_t, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipMemcpyAsync(tri_out, ctx->d_tri, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return PT_OK;
+}
+
+int pt_download_accum(pt_ctx* ctx, float* accum) {
+  if (!ctx || !accum) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
+  CK(hipMemcpyAsync(accum, ctx->d_accum, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return PT_OK;
+}
+
+int pt_upload_accum(pt_ctx* ctx, const float* accum) {
+  if (!ctx || !accum) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
+  CK(hipMemcpyAsync(ctx->d_accum, accum, bytes, hipMemcpyHostToDevice, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return PT_OK;
+}
+
+int pt_clear_accum(pt_ctx* ctx) {
+  if (!ctx) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  CK(hipMemsetAsync(ctx->d_accum, 0, (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4), ctx->stream));
+  return PT_OK;
+}
+
+int pt_accum_device_ptr(pt_ctx* ctx, void** dptr) {
+  if (!ctx || !dptr) return PT_E_INVALID;
+  *dptr = ctx->d_accum;
+  return PT_OK;
+}
+
+int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out) {
+  if (!ctx || !rgb_out || !(limit > 0.0f)) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  const int n = ctx->cfg.width * ctx->cfg.height;
+  if (!ctx->d_rgb) CK(hipMalloc(&ctx->d_rgb, (size_t)n * 3 * sizeof(float)));
+  CK(launchTonemap(ctx->d_accum, ctx->d_rgb, n, limit, gamma, ctx->stream));
+  CK(hipMemcpyAsync(rgb_out, ctx->d_rgb, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return PT_OK;
+}
+
+static PackParams packParams(const pt_ctx* ctx, int rank, int world) {
+  PackParams p;
+  p.width = ctx->cfg.width;
+  p.height = ctx->cfg.height;
+  p.shardSize = ctx->shardSize;
+  p.shardsX = ctx->shardsX;
+  p.rank = rank;
+  p.world = world;
+  const int numShards = ctx->shardsX * ctx->shardsY;
+  const long owned = (numShards - rank + world - 1) / world;
+  p.count = owned * (long)ctx->shardSize * ctx->shardSize;
+  return p;
+}
+
+int pt_owned_pixel_count(pt_ctx* ctx, int rank, int world, int64_t* count) {
+  if (!ctx || !count || world < 1 || rank < 0 || rank >= world) return PT_E_INVALID;
+  *count = packParams(ctx, rank, world).count;
+  return PT_OK;
+}
+
+int pt_pack_owned(pt_ctx* ctx, void* dpacked) {
+  if (!ctx || !dpacked) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  PackParams p = packParams(ctx, ctx->cfg.tile_rank, ctx->cfg.tile_world);
+  CK(launchPack(p, ctx->d_accum, reinterpret_cast<float4*>(dpacked), ctx->stream));
+  return PT_OK;
+}
+
+int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked) {
+  if (!ctx || !dpacked || world < 1 || rank < 0 || rank >= world) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  PackParams p = packParams(ctx, rank, world);
+  CK(launchUnpack(p, ctx->d_accum, reinterpret_cast<const float4*>(dpacked), ctx->stream));
+  return PT_OK;
+}
+
+int pt_set_stream(pt_ctx* ctx, void* s) {
+  if (!ctx) return PT_E_INVALID;
+  ctx->stream = s ? reinterpret_cast<hipStream_t>(s) : ctx->own;
+  return PT_OK;
+}
+
+int pt_synchronize(pt_ctx* ctx) {
+  if (!ctx) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  CK(hipStreamSynchronize(ctx->stream));
+  return PT_OK;
+}
+
+int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
+  if (!ctx || !st) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  CK(hipStreamSynchronize(ctx->stream));
+  unsigned long long h[5];
+  CK(hipMemcpy(h, ctx->d_ctl + 64, sizeof(h), hipMemcpyDeviceToHost));
+  std::memset(st, 0, sizeof(*st));
+  st->rays = h[0];
+  st->node_fetch = h[1];
+  st->tri_fetch = h[2];
+  st->mat_fetch = h[3];
+  st->tex_fetch = h[4];
+  st->kernel_ms = 0.0f;
+  st->kernel_ms_total = 0.0f;
+  for (int k = 0; k < ctx->launches; k++) {
+    float ms = 0.0f;
+    CK(hipEventElapsedTime(&ms, ctx->evs[2 * k], ctx->evs[2 * k + 1]));
+    st->kernel_ms_total += ms;
+    st->kernel_ms = ms;
+  }
+  st->launches = ctx->launches;
+  st->max_stack = ctx->maxStack;
+  return PT_OK;
+}
+
+int pt_reset_stats(pt_ctx* ctx) {
+  if (!ctx) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  CK(hipStreamSynchronize(ctx->stream));
+  CK(hipMemset(ctx->d_ctl + 64, 0, 64));
+  ctx->launches = 0;
+  return PT_OK;
+}
+
+}  // extern "C"

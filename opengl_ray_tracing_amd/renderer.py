@@ -1,0 +1,180 @@
+"""Renderer: the per-frame loop of the reference (display(), OpenglRayTracing/main.cpp:558-603)
+driving the MI355X kernels through the C ABI (include/pt_abi.h).
+
+    r = Renderer(1920, 1080, integrator="lambert")
+    r.upload_scene(tris, nodes); r.upload_env(hdr)
+    eye, rot = orbit_camera(0, 0, 4)
+    for frame in range(n): r.render_frame(eye, rot, frame)
+    img = r.accum()          # (h, w, 4) running mean, row 0 = bottom row (GL)
+
+Nothing here has a CPU path: every call goes to libpt.so and raises if the
+native library or the GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+
+INTEGRATORS = {
+    "lambert": 0, "lambert_o": 0,           # OpenglRayTracing/shaders/pass1.fsh
+    "disney": 1, "disney_uniform_d": 1,     # DisneyBRDF/shaders/pass1.fsh
+    "mis": 2, "disney_mis_sobol_is": 2,     # ImportanceSampling_LowDiscrepancySequence/shaders/pass1.fsh
+    "basic": 3, "basic_cpu_compat": 3,      # BasicRayTracingWithC++/main.cpp
+}
+FLAG_NO_CULL = 0x1
+FLAG_CLOSEST_SHADOW = 0x2
+FLAG_COUNT_FETCHES = 0x4
+
+
+@dataclass
+class FrameStats:
+    rays: int
+    node_fetch: int
+    tri_fetch: int
+    mat_fetch: int
+    tex_fetch: int
+    kernel_ms: float
+    kernel_ms_total: float
+    launches: int
+    max_stack: int
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_native.c_float_p)
+
+
+def device_count() -> int:
+    n = C.c_int()
+    _native.load().pt_device_count(C.byref(n))
+    return n.value
+
+
+class Renderer:
+    def __init__(self, width: int, height: int, integrator="lambert", max_bounce: int = -1, device: int = 0,
+                 tile_rank: int = 0, tile_world: int = 1, tile_size: int = 32, flags: int = 0,
+                 basic_samples: int = 128, basic_seed: int = 0):
+        self._lib = _native.load()
+        cfg = _native.PtConfig()
+        cfg.width, cfg.height = int(width), int(height)
+        cfg.integrator = INTEGRATORS[integrator] if isinstance(integrator, str) else int(integrator)
+        cfg.max_bounce = int(max_bounce)
+        cfg.device_id = int(device)
+        cfg.tile_rank, cfg.tile_world, cfg.tile_size = int(tile_rank), int(tile_world), int(tile_size)
+        cfg.flags = int(flags)
+        cfg.basic_samples = int(basic_samples)
+        cfg.basic_seed = int(basic_seed) & 0xFFFFFFFF
+        h = C.c_void_p()
+        _native.check(self._lib.pt_create(C.byref(h), C.byref(cfg)), None, "pt_create")
+        self._h = h
+        self.width, self.height = cfg.width, cfg.height
+        self.integrator = cfg.integrator
+        self.tile_rank, self.tile_world = cfg.tile_rank, cfg.tile_world
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pt_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _ck(self, rc, what):
+        _native.check(rc, self._h, what)
+
+    def upload_scene(self, tris: np.ndarray, nodes: np.ndarray):
+        t = np.ascontiguousarray(tris, np.float32).reshape(-1, 36)
+        n = np.ascontiguousarray(nodes, np.float32).reshape(-1, 12)
+        self._ck(self._lib.pt_upload_scene(self._h, _fp(t), t.shape[0], _fp(n), n.shape[0]), "pt_upload_scene")
+
+    def upload_env(self, hdr, cache=None):
+        if hdr is None:
+            self._ck(self._lib.pt_upload_env(self._h, None, 0, 0, None), "pt_upload_env")
+            return
+        h = np.ascontiguousarray(hdr, np.float32)
+        hh, ww = h.shape[:2]
+        c = None if cache is None else np.ascontiguousarray(cache, np.float32)
+        self._ck(self._lib.pt_upload_env(self._h, _fp(h), ww, hh, None if c is None else _fp(c)), "pt_upload_env")
+
+    def upload_shapes(self, shapes: np.ndarray):
+        s = np.ascontiguousarray(shapes, np.float32).reshape(-1, 24)
+        self._ck(self._lib.pt_upload_shapes(self._h, _fp(s), s.shape[0]), "pt_upload_shapes")
+
+    def render_frame(self, eye, camera_rotate, frame_counter: int, download: bool = False, sync: bool = True):
+        e = np.ascontiguousarray(eye, np.float32)
+        r = np.ascontiguousarray(camera_rotate, np.float32).reshape(16)
+        if not sync:
+            self._ck(self._lib.pt_render_frame_async(self._h, _fp(e), _fp(r), int(frame_counter) & 0xFFFFFFFF),
+                     "pt_render_frame_async")
+            return None
+        out = np.empty((self.height, self.width, 4), np.float32) if download else None
+        self._ck(self._lib.pt_render_frame(self._h, _fp(e), _fp(r), int(frame_counter) & 0xFFFFFFFF,
+                                           None if out is None else _fp(out)), "pt_render_frame")
+        return out
+
+    def trace_closest(self, rays: np.ndarray):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+        n = r.shape[0]
+        t = np.empty(n, np.float32)
+        tri = np.empty(n, np.int32)
+        self._ck(self._lib.pt_trace_closest(self._h, _fp(r), n, _fp(t), tri.ctypes.data_as(_native.c_int_p)),
+                 "pt_trace_closest")
+        return t, tri
+
+    def accum(self) -> np.ndarray:
+        out = np.empty((self.height, self.width, 4), np.float32)
+        self._ck(self._lib.pt_download_accum(self._h, _fp(out)), "pt_download_accum")
+        return out
+
+    def set_accum(self, a: np.ndarray):
+        a = np.ascontiguousarray(a, np.float32).reshape(self.height, self.width, 4)
+        self._ck(self._lib.pt_upload_accum(self._h, _fp(a)), "pt_upload_accum")
+
+    def clear(self):
+        self._ck(self._lib.pt_clear_accum(self._h), "pt_clear_accum")
+
+    def accum_device_ptr(self) -> int:
+        p = C.c_void_p()
+        self._ck(self._lib.pt_accum_device_ptr(self._h, C.byref(p)), "pt_accum_device_ptr")
+        return p.value
+
+    def tonemap(self, limit: float = 1.5, gamma: float = 0.0) -> np.ndarray:
+        out = np.empty((self.height, self.width, 3), np.float32)
+        self._ck(self._lib.pt_tonemap(self._h, float(limit), float(gamma), _fp(out)), "pt_tonemap")
+        return out
+
+    def owned_pixel_count(self, rank=None, world=None) -> int:
+        c = C.c_int64()
+        rank = self.tile_rank if rank is None else rank
+        world = self.tile_world if world is None else world
+        self._ck(self._lib.pt_owned_pixel_count(self._h, int(rank), int(world), C.byref(c)), "pt_owned_pixel_count")
+        return c.value
+
+    def pack_owned(self, dptr: int):
+        self._ck(self._lib.pt_pack_owned(self._h, C.c_void_p(dptr)), "pt_pack_owned")
+
+    def unpack_rank(self, rank: int, world: int, dptr: int):
+        self._ck(self._lib.pt_unpack_rank(self._h, int(rank), int(world), C.c_void_p(dptr)), "pt_unpack_rank")
+
+    def set_stream(self, stream_ptr: int | None):
+        self._ck(self._lib.pt_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None), "pt_set_stream")
+
+    def synchronize(self):
+        self._ck(self._lib.pt_synchronize(self._h), "pt_synchronize")
+
+    def stats(self) -> FrameStats:
+        s = _native.PtFrameStats()
+        self._ck(self._lib.pt_get_stats(self._h, C.byref(s)), "pt_get_stats")
+        return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
+                          s.kernel_ms_total, s.launches, s.max_stack)
+
+    def reset_stats(self):
+        self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

@@ -1,0 +1,170 @@
+"""ctypes wrapper of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference path (oracle/pt_oracle.c). Imported by
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg only, and
+there only as the checker / the CPU baseline, never as the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+LIB_PATH = ROOT / "oracle" / "liboracle.so"
+
+c_float_p = C.POINTER(C.c_float)
+
+
+class OrcScene(C.Structure):
+    _fields_ = [("tris", c_float_p), ("nTriangles", C.c_int), ("nodes", c_float_p), ("nNodes", C.c_int),
+                ("hdr", c_float_p), ("cache", c_float_p), ("hdrW", C.c_int), ("hdrH", C.c_int),
+                ("hdrResolution", C.c_int), ("shapes", c_float_p), ("nShapes", C.c_int)]
+
+
+class OrcFrame(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("integrator", C.c_int), ("maxBounce", C.c_int),
+                ("frameCounter", C.c_uint32), ("eye", C.c_float * 3), ("cameraRotate", C.c_float * 16),
+                ("basicSamples", C.c_int), ("basicSeed", C.c_uint32)]
+
+
+class OrcCounters(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("nodes", C.c_uint64), ("tris", C.c_uint64), ("mats", C.c_uint64),
+                ("texels", C.c_uint64)]
+
+
+@dataclass
+class Counters:
+    rays: int
+    nodes: int
+    tris: int
+    mats: int
+    texels: int
+
+    @property
+    def bytes(self) -> int:
+        """B = 48 F_node + 72 F_tri + 72 F_mat + 12 F_tex."""
+        return 48 * self.nodes + 72 * self.tris + 72 * self.mats + 12 * self.texels
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            from opengl_ray_tracing_amd import _build
+            _build.build_oracle()
+        lib = C.CDLL(str(LIB_PATH))
+        lib.orc_render_pixels.argtypes = [C.POINTER(OrcScene), C.POINTER(OrcFrame), C.POINTER(C.c_int), C.c_int,
+                                          c_float_p, C.c_int, C.POINTER(OrcCounters)]
+        lib.orc_render_pixels.restype = C.c_int
+        lib.orc_trace_closest.argtypes = [C.POINTER(OrcScene), c_float_p, C.c_int, c_float_p, C.POINTER(C.c_int),
+                                          C.c_int, C.POINTER(OrcCounters)]
+        lib.orc_trace_closest.restype = C.c_int
+        lib.orc_wang_hash.argtypes = [C.c_uint32]
+        lib.orc_wang_hash.restype = C.c_uint32
+        lib.orc_sobol.argtypes = [C.c_uint32, C.c_uint32]
+        lib.orc_sobol.restype = C.c_float
+        lib.orc_pixel_rng.argtypes = [C.c_int, C.c_int, C.c_uint32, C.c_int, c_float_p]
+        lib.orc_pixel_rng.restype = None
+        lib.orc_hdr_cache.argtypes = [c_float_p, C.c_int, C.c_int, c_float_p]
+        lib.orc_hdr_cache.restype = C.c_int
+        _lib = lib
+    return _lib
+
+
+INTEG = {"lambert": 0, "disney": 1, "mis": 2, "basic": 3}
+
+
+class Oracle:
+    """Holds the scene arrays alive while the C structs point at them."""
+
+    def __init__(self, tris=None, nodes=None, hdr=None, cache=None, shapes=None):
+        self.lib = load()
+        self._keep = []
+        s = OrcScene()
+
+        def fp(a):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(a, np.float32)
+            self._keep.append(a)
+            return a.ctypes.data_as(c_float_p)
+
+        if tris is not None:
+            s.tris, s.nTriangles = fp(tris), int(np.asarray(tris).reshape(-1, 36).shape[0])
+        if nodes is not None:
+            s.nodes, s.nNodes = fp(nodes), int(np.asarray(nodes).reshape(-1, 12).shape[0])
+        if hdr is not None:
+            h, w = hdr.shape[:2]
+            if cache is None:
+                cache = hdr_cache(hdr)
+            s.hdr, s.cache, s.hdrW, s.hdrH, s.hdrResolution = fp(hdr), fp(cache), w, h, w
+        if shapes is not None:
+            s.shapes, s.nShapes = fp(shapes), int(np.asarray(shapes).reshape(-1, 24).shape[0])
+        self.scene = s
+
+    def render(self, width, height, integrator, frame, eye=None, rot=None, accum=None, pixels=None,
+               max_bounce=-1, threads=8, basic_samples=128, basic_seed=0):
+        f = OrcFrame()
+        f.width, f.height = width, height
+        f.integrator = INTEG[integrator] if isinstance(integrator, str) else integrator
+        f.maxBounce = max_bounce
+        f.frameCounter = frame & 0xFFFFFFFF
+        if eye is not None:
+            f.eye[:] = [float(x) for x in eye]
+        if rot is not None:
+            f.cameraRotate[:] = [float(x) for x in np.asarray(rot).reshape(16)]
+        f.basicSamples = basic_samples
+        f.basicSeed = basic_seed
+        if accum is None:
+            accum = np.zeros((height, width, 4), np.float32)
+        assert accum.dtype == np.float32 and accum.flags.c_contiguous and accum.shape == (height, width, 4)
+        cnt = OrcCounters()
+        if pixels is not None:
+            px = np.ascontiguousarray(pixels, np.int32).reshape(-1, 2)
+            pp, n = px.ctypes.data_as(C.POINTER(C.c_int)), px.shape[0]
+        else:
+            pp, n = None, 0
+        rc = self.lib.orc_render_pixels(C.byref(self.scene), C.byref(f), pp, n, accum.ctypes.data_as(c_float_p),
+                                        threads, C.byref(cnt))
+        assert rc == 0, rc
+        return accum, Counters(cnt.rays, cnt.nodes, cnt.tris, cnt.mats, cnt.texels)
+
+    def trace_closest(self, rays, brute=False):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+        n = r.shape[0]
+        t = np.empty(n, np.float32)
+        tri = np.empty(n, np.int32)
+        cnt = OrcCounters()
+        rc = self.lib.orc_trace_closest(C.byref(self.scene), r.ctypes.data_as(c_float_p), n,
+                                        t.ctypes.data_as(c_float_p), tri.ctypes.data_as(C.POINTER(C.c_int)),
+                                        int(brute), C.byref(cnt))
+        assert rc == 0
+        return t, tri, Counters(cnt.rays, cnt.nodes, cnt.tris, cnt.mats, cnt.texels)
+
+
+def wang_hash(x: int) -> int:
+    return load().orc_wang_hash(x & 0xFFFFFFFF)
+
+
+def sobol(d: int, i: int) -> float:
+    return load().orc_sobol(d, i)
+
+
+def pixel_rng(px, py, frame, n):
+    out = np.empty(n, np.float32)
+    load().orc_pixel_rng(px, py, frame, n, out.ctypes.data_as(c_float_p))
+    return out
+
+
+def hdr_cache(hdr):
+    hdr = np.ascontiguousarray(hdr, np.float32)
+    h, w = hdr.shape[:2]
+    out = np.zeros((h, w, 3), np.float32)
+    assert load().orc_hdr_cache(hdr.ctypes.data_as(c_float_p), w, h, out.ctypes.data_as(c_float_p)) == 0
+    return out
