@@ -143,6 +143,12 @@ int pt_synchronize(pt_ctx* ctx);
 int pt_get_stats(pt_ctx* ctx, pt_frame_stats* stats);   /* synchronises the stream */
 int pt_reset_stats(pt_ctx* ctx);
 
+/* Diagnostics: evaluate one include/pt_fmath.h function (0 sin, 1 cos, 2 atan2(x,y),
+ * 3 asin, 4 log, 5 exp, 6 pow(x,y)) over n inputs on the host CPU or on the
+ * context's GPU; the two must agree bit for bit. */
+int pt_fmath_host(int fn, const float* x, const float* y, int n, float* out);
+int pt_fmath_device(pt_ctx* ctx, int fn, const float* x, const float* y, int n, float* out);
+
 #ifdef __cplusplus
 }
 #endif

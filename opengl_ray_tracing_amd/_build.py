@@ -35,8 +35,10 @@ CXX_FLAGS = ["-O2", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-fast-math"
              "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"]
 
 SOURCES = {
-    "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h"]),
-    "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h"]),
+    "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h",
+                                                       INCLUDE / "pt_fmath.h"]),
+    "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
+                                                       INCLUDE / "pt_fmath.h"]),
     "scene.o": ("cxx", CSRC / "scene.cpp", [INCLUDE / "pt_scene.h"]),
 }
 
@@ -81,7 +83,7 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
 
 def build_oracle(force: bool = False) -> Path:
     """Test infrastructure only (see oracle/pt_oracle.h)."""
-    src = [ORACLE_DIR / "pt_oracle.c", ORACLE_DIR / "pt_oracle.h"]
+    src = [ORACLE_DIR / "pt_oracle.c", ORACLE_DIR / "pt_oracle.h", ORACLE_DIR / "Makefile", INCLUDE / "pt_fmath.h"]
     if force or _stale(ORACLE_LIB, src):
         _run(["make", "-s", "-C", str(ORACLE_DIR), "-B" if force else "all"])
     return ORACLE_LIB

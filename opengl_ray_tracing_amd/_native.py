@@ -68,6 +68,8 @@ SIGNATURES = {
     "pt_synchronize": (C.c_int, [C.c_void_p]),
     "pt_get_stats": (C.c_int, [C.c_void_p, C.POINTER(PtFrameStats)]),
     "pt_reset_stats": (C.c_int, [C.c_void_p]),
+    "pt_fmath_host": (C.c_int, [C.c_int, c_float_p, c_float_p, C.c_int, c_float_p]),
+    "pt_fmath_device": (C.c_int, [C.c_void_p, C.c_int, c_float_p, c_float_p, C.c_int, c_float_p]),
     # pt_scene.h
     "pt_material_default": (None, [C.POINTER(PtMaterial)]),
     "pt_scene_create": (C.c_int, [C.POINTER(C.c_void_p)]),

@@ -4,8 +4,8 @@
 // so the GPU and the CPU checker round identically wherever the hardware
 // operations are correctly rounded (+,-,*,/,sqrt; the build uses
 // -ffp-contract=off and IEEE fp32 division/sqrt). Transcendentals come from
-// ROCm's ocml and may differ by an ulp from glibc: parity is stated with a
-// tolerance for them.
+// include/pt_fmath.h (explicit-fma polynomials), shared by the CPU checker, so
+// they round identically too.
 //
 // IS = ImportanceSampling_LowDiscrepancySequence/shaders/pass1.fsh,
 // D = DisneyBRDF/shaders/pass1.fsh, O = OpenglRayTracing/shaders/pass1.fsh.
@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pt_fmath.h"
 #include "pt_kernels.h"
 
 #define PT_PI 3.1415926f          // IS:23
@@ -129,7 +130,7 @@ __device__ __forceinline__ float4 texNearest(const float4* img, int w, int h, fl
 }
 // SampleSphericalMap IS:175-181 / toSphericalCoord IS:638-644
 __device__ __forceinline__ void toSpherical(V3 v, float& u, float& w) {
-  float a = atan2f(v.z, v.x), b = asinf(v.y);
+  float a = ptm_atan2f(v.z, v.x), b = ptm_asinf(v.y);
   a = a / (2.0f * PT_PI);
   b = b / PT_PI;
   a = a + 0.5f;
@@ -164,7 +165,7 @@ __device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
   y = 1.0f - y;
   float phi = 2.0f * PT_PI * (x - 0.5f);
   float theta = PT_PI * (y - 0.5f);
-  return v3(cosf(theta) * cosf(phi), sinf(theta), cosf(theta) * sinf(phi));
+  return v3(ptm_cosf(theta) * ptm_cosf(phi), ptm_sinf(theta), ptm_cosf(theta) * ptm_sinf(phi));
 }
 // hdrPdf IS:655-666 (sin of the elevation: reference quirk kept)
 __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
@@ -172,7 +173,7 @@ __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
   toSpherical(normalize(L), u, w);
   float pdf = e.cache ? texNearest(e.cache, e.w, e.h, u, w).z : 0.0f;
   float theta = PT_PI * (0.5f - w);
-  float sin_theta = fmaxf(sinf(theta), 1e-10f);
+  float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
   float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
   return pdf * p_convert;
 }
@@ -187,7 +188,7 @@ __device__ __forceinline__ float GTR1(float NdotH, float a) {
   if (a >= 1.0f) return 1.0f / PT_PI;
   float a2 = a * a;
   float t = 1.0f + (a2 - 1.0f) * NdotH * NdotH;
-  return (a2 - 1.0f) / (PT_PI * logf(a2) * t);
+  return (a2 - 1.0f) / (PT_PI * ptm_logf(a2) * t);
 }
 __device__ __forceinline__ float GTR2(float NdotH, float a) {
   float a2 = a * a;
@@ -335,25 +336,25 @@ __device__ __forceinline__ V3 sampleHemisphereRand(uint32_t& seed) {
   float z = randf(seed);
   float r = fmaxf(0.0f, sqrtf(1.0f - z * z));
   float phi = 2.0f * PT_PI * randf(seed);
-  return v3(r * cosf(phi), r * sinf(phi), z);
+  return v3(r * ptm_cosf(phi), r * ptm_sinf(phi), z);
 }
 // SampleCosineHemisphere IS:485-496
 __device__ __forceinline__ V3 sampleCosine(float xi_1, float xi_2, V3 N) {
   float r = sqrtf(xi_1);
   float theta = xi_2 * 2.0f * PT_PI;
-  float x = r * cosf(theta);
-  float y = r * sinf(theta);
+  float x = r * ptm_cosf(theta);
+  float y = r * ptm_sinf(theta);
   float z = sqrtf(1.0f - x * x - y * y);
   return toNormalHemisphere(v3(x, y, z), N);
 }
 // SampleGTR2 IS:499-516 / SampleGTR1 IS:519-536
 __device__ __forceinline__ V3 sampleGTR(float xi_1, float xi_2, V3 V, V3 N, float alpha, bool gtr1) {
   float phi_h = 2.0f * PT_PI * xi_1;
-  float sin_phi_h = sinf(phi_h);
-  float cos_phi_h = cosf(phi_h);
+  float sin_phi_h = ptm_sinf(phi_h);
+  float cos_phi_h = ptm_cosf(phi_h);
   float cos_theta_h;
   if (gtr1)
-    cos_theta_h = sqrtf((1.0f - powf(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));
+    cos_theta_h = sqrtf((1.0f - ptm_powf(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));
   else
     cos_theta_h = sqrtf((1.0f - xi_2) / (1.0f + (alpha * alpha - 1.0f) * xi_2));
   float sin_theta_h = sqrtf(fmaxf(0.0f, 1.0f - cos_theta_h * cos_theta_h));

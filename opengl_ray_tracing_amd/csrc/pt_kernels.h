@@ -83,6 +83,7 @@ hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull)
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s);
 hipError_t launchPack(const PackParams& p, const float4* accum, float4* packed, hipStream_t s);
+hipError_t launchFmath(int fn, const float* x, const float* y, int n, float* out, hipStream_t s);
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float4* packed, hipStream_t s);
 
 }  // namespace pt

@@ -574,9 +574,9 @@ __global__ void tonemapKernel(const float4* accum, float* rgb, int n, float limi
   float s = 1.0f / (1.0f + lum / limit);
   float r = c.x * s, g = c.y * s, b = c.z * s;
   if (gamma > 0.0f) {
-    r = powf(r, 1.0f / gamma);
-    g = powf(g, 1.0f / gamma);
-    b = powf(b, 1.0f / gamma);
+    r = ptm_powf(r, 1.0f / gamma);
+    g = ptm_powf(g, 1.0f / gamma);
+    b = ptm_powf(b, 1.0f / gamma);
   }
   rgb[3 * i] = r;
   rgb[3 * i + 1] = g;
@@ -605,6 +605,23 @@ __global__ void unpackKernel(PackParams p, float4* accum, const float4* packed) 
   if (k >= p.count) return;
   int px, py;
   if (packedPixel(p, k, px, py)) accum[(size_t)py * p.width + px] = packed[k];
+}
+
+// include/pt_fmath.h evaluated on the device (diagnostics; bit-equality with the host)
+__device__ __forceinline__ float fmathEval(int fn, float x, float y) {
+  switch (fn) {
+    case 0: return ptm_sinf(x);
+    case 1: return ptm_cosf(x);
+    case 2: return ptm_atan2f(x, y);
+    case 3: return ptm_asinf(x);
+    case 4: return ptm_logf(x);
+    case 5: return ptm_expf(x);
+    default: return ptm_powf(x, y);
+  }
+}
+__global__ void fmathKernel(int fn, const float* x, const float* y, int n, float* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = fmathEval(fn, x[i], y ? y[i] : 0.0f);
 }
 
 }  // namespace pt
@@ -658,6 +675,12 @@ hipError_t launchBasic(const BasicParams& p, hipStream_t s) {
 
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s) {
   hipLaunchKernelGGL(tonemapKernel, dim3((n + 255) / 256), dim3(256), 0, s, accum, rgb, n, limit, gamma);
+  return hipGetLastError();
+}
+
+hipError_t launchFmath(int fn, const float* x, const float* y, int n, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fmathKernel, dim3((n + 255) / 256), dim3(256), 0, s, fn, x, y, n, out);
   return hipGetLastError();
 }
 

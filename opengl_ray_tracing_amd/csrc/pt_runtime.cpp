@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "pt_abi.h"
+#include "pt_fmath.h"
 #include "pt_kernels.h"
 #include "pt_scene.h"
 
@@ -576,6 +577,45 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   }
   st->launches = ctx->launches;
   st->max_stack = ctx->maxStack;
+  return PT_OK;
+}
+
+static float fmathHost(int fn, float x, float y) {
+  switch (fn) {
+    case 0: return ptm_sinf(x);
+    case 1: return ptm_cosf(x);
+    case 2: return ptm_atan2f(x, y);
+    case 3: return ptm_asinf(x);
+    case 4: return ptm_logf(x);
+    case 5: return ptm_expf(x);
+    default: return ptm_powf(x, y);
+  }
+}
+
+int pt_fmath_host(int fn, const float* x, const float* y, int n, float* out) {
+  if (fn < 0 || fn > 6 || n < 0 || (n > 0 && (!x || !out))) return PT_E_INVALID;
+  for (int i = 0; i < n; i++) out[i] = fmathHost(fn, x[i], y ? y[i] : 0.0f);
+  return PT_OK;
+}
+
+int pt_fmath_device(pt_ctx* ctx, int fn, const float* x, const float* y, int n, float* out) {
+  if (!ctx || fn < 0 || fn > 6 || n < 0 || (n > 0 && (!x || !out))) return PT_E_INVALID;
+  if (n == 0) return PT_OK;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  const size_t b = (size_t)n * sizeof(float);
+  CK(hipMalloc(&dx, b));
+  CK(hipMalloc(&dy, b));
+  CK(hipMalloc(&dout, b));
+  CK(hipMemcpy(dx, x, b, hipMemcpyHostToDevice));
+  if (y) CK(hipMemcpy(dy, y, b, hipMemcpyHostToDevice));
+  else CK(hipMemset(dy, 0, b));
+  CK(launchFmath(fn, dx, dy, n, dout, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  CK(hipMemcpy(out, dout, b, hipMemcpyDeviceToHost));
+  CK(hipFree(dx));
+  CK(hipFree(dy));
+  CK(hipFree(dout));
   return PT_OK;
 }
 

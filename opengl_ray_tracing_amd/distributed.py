@@ -1,0 +1,85 @@
+"""Multi-GPU frame sharding: screen tiles of `shard` x `shard`
+pixels dealt round-robin over the ranks (tile t belongs to rank t % world),
+one process per GPU, one gather of the packed shards to rank 0 per presented
+frame over RCCL/xGMI.
+
+Every pixel's value depends only on (pixel, frameCounter) and its own running
+mean (pass1.fsh:73-76, :118-122, :868-871), so the reassembled frame is
+bit-identical to a single-GPU render. The packed order (tile, row, column)
+matches the kernels in csrc/pt_kernels.hip (packKernel / unpackKernel).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_grid(width: int, height: int, shard: int = 32):
+    return (width + shard - 1) // shard, (height + shard - 1) // shard
+
+
+def owned_tiles(width: int, height: int, rank: int, world: int, shard: int = 32) -> np.ndarray:
+    sx, sy = shard_grid(width, height, shard)
+    return np.arange(rank, sx * sy, world, dtype=np.int64)
+
+
+def packed_count(width: int, height: int, rank: int, world: int, shard: int = 32) -> int:
+    return int(owned_tiles(width, height, rank, world, shard).size) * shard * shard
+
+
+def packed_coords(width: int, height: int, rank: int, world: int, shard: int = 32):
+    """(px, py, valid) of every packed slot, in the kernels' (tile, row, col) order."""
+    sx, _ = shard_grid(width, height, shard)
+    g = owned_tiles(width, height, rank, world, shard)
+    within = np.arange(shard * shard, dtype=np.int64)
+    gy, gx = (g // sx)[:, None], (g % sx)[:, None]
+    px = (gx * shard + within[None] % shard).ravel()
+    py = (gy * shard + within[None] // shard).ravel()
+    valid = (px < width) & (py < height)
+    return px, py, valid
+
+
+def owned_pixels(width: int, height: int, rank: int, world: int, shard: int = 32) -> np.ndarray:
+    px, py, v = packed_coords(width, height, rank, world, shard)
+    return np.stack([px[v], py[v]], 1).astype(np.int32)
+
+
+def pack(accum: np.ndarray, rank: int, world: int, shard: int = 32) -> np.ndarray:
+    h, w = accum.shape[:2]
+    px, py, v = packed_coords(w, h, rank, world, shard)
+    out = np.zeros((px.size, accum.shape[2]), accum.dtype)
+    out[v] = accum[py[v], px[v]]
+    return out
+
+
+def unpack(accum: np.ndarray, packed: np.ndarray, rank: int, world: int, shard: int = 32) -> None:
+    h, w = accum.shape[:2]
+    px, py, v = packed_coords(w, h, rank, world, shard)
+    accum[py[v], px[v]] = packed[v]
+
+
+class FrameGather:
+    """RCCL gather of every rank's shard of a Renderer's accumulation to rank 0.
+
+    Device buffers are torch tensors (torch is the allocator/collective
+    plumbing here); the pack/unpack kernels and the renderer run on torch's
+    current stream so the collective orders after them.
+    """
+
+    def __init__(self, renderer, rank: int, world: int, device):
+        import torch
+        import torch.distributed as dist
+
+        self.r, self.rank, self.world, self.dist = renderer, rank, world, dist
+        counts = [renderer.owned_pixel_count(k, world) for k in range(world)]
+        self.maxc = max(counts)
+        self.send = torch.zeros((self.maxc, 4), dtype=torch.float32, device=device)
+        self.recv = [torch.zeros((self.maxc, 4), dtype=torch.float32, device=device) for _ in range(world)] \
+            if rank == 0 else None
+        renderer.set_stream(torch.cuda.current_stream(device).cuda_stream)
+
+    def __call__(self):
+        self.r.pack_owned(self.send.data_ptr())
+        self.dist.gather(self.send, gather_list=self.recv, dst=0)
+        if self.rank == 0:
+            for k in range(1, self.world):
+                self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())

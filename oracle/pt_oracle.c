@@ -13,6 +13,7 @@
  * B = BasicRayTracingWithC++/main.cpp, H = OpenglRayTracing/main.cpp.
  */
 #include "pt_oracle.h"
+#include "pt_fmath.h" /* the numerics contract for transcendentals (include/) */
 
 #include <math.h>
 #include <stdlib.h>
@@ -289,7 +290,7 @@ static v3 tex_nearest(Ctx* cx, const float* img, float u, float v) {
 }
 /* SampleSphericalMap IS:175-181 == toSphericalCoord IS:638-644 */
 static void toSpherical(v3 v, float* u, float* w) {
-  float a = atan2f(v.z, v.x), b = asinf(v.y);
+  float a = ptm_atan2f(v.z, v.x), b = ptm_asinf(v.y);
   a = a / (2.0f * PI);
   b = b / PI;
   a = a + 0.5f;
@@ -315,7 +316,7 @@ static v3 SampleHdrDir(Ctx* cx, float xi1, float xi2) {
   float x = xy.x, y = 1.0f - xy.y;
   float phi = 2.0f * PI * (x - 0.5f);
   float theta = PI * (y - 0.5f);
-  return V3(cosf(theta) * cosf(phi), sinf(theta), cosf(theta) * sinf(phi));
+  return V3(ptm_cosf(theta) * ptm_cosf(phi), ptm_sinf(theta), ptm_cosf(theta) * ptm_sinf(phi));
 }
 /* hdrPdf IS:655-666 (sin of the elevation: reference bug kept) */
 static float hdrPdf(Ctx* cx, v3 L, int hdrResolution) {
@@ -323,7 +324,7 @@ static float hdrPdf(Ctx* cx, v3 L, int hdrResolution) {
   toSpherical(normalize(L), &u, &w);
   float pdf = tex_nearest(cx, cx->s->cache, u, w).z;
   float theta = PI * (0.5f - w);
-  float sin_theta = fmaxf(sinf(theta), 1e-10f);
+  float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
   float p_convert = (float)(hdrResolution * hdrResolution / 2) / (2.0f * PI * PI * sin_theta);
   return pdf * p_convert;
 }
@@ -338,7 +339,7 @@ static float GTR1(float NdotH, float a) {
   if (a >= 1.0f) return 1.0f / PI;
   float a2 = a * a;
   float t = 1.0f + (a2 - 1.0f) * NdotH * NdotH;
-  return (a2 - 1.0f) / (PI * logf(a2) * t);
+  return (a2 - 1.0f) / (PI * ptm_logf(a2) * t);
 }
 static float GTR2(float NdotH, float a) {
   float a2 = a * a;
@@ -486,22 +487,22 @@ static v3 SampleHemisphereRand(uint32_t* seed) {
   float z = randf(seed);
   float r = fmaxf(0.0f, sqrtf(1.0f - z * z));
   float phi = 2.0f * PI * randf(seed);
-  return V3(r * cosf(phi), r * sinf(phi), z);
+  return V3(r * ptm_cosf(phi), r * ptm_sinf(phi), z);
 }
 /* SampleCosineHemisphere IS:485-496 */
 static v3 SampleCosineHemisphere(float xi_1, float xi_2, v3 N) {
   float r = sqrtf(xi_1);
   float theta = xi_2 * 2.0f * PI;
-  float x = r * cosf(theta);
-  float y = r * sinf(theta);
+  float x = r * ptm_cosf(theta);
+  float y = r * ptm_sinf(theta);
   float z = sqrtf(1.0f - x * x - y * y);
   return toNormalHemisphere(V3(x, y, z), N);
 }
 /* SampleGTR2 IS:499-516 */
 static v3 SampleGTR2(float xi_1, float xi_2, v3 V, v3 N, float alpha) {
   float phi_h = 2.0f * PI * xi_1;
-  float sin_phi_h = sinf(phi_h);
-  float cos_phi_h = cosf(phi_h);
+  float sin_phi_h = ptm_sinf(phi_h);
+  float cos_phi_h = ptm_cosf(phi_h);
   float cos_theta_h = sqrtf((1.0f - xi_2) / (1.0f + (alpha * alpha - 1.0f) * xi_2));
   float sin_theta_h = sqrtf(fmaxf(0.0f, 1.0f - cos_theta_h * cos_theta_h));
   v3 H = V3(sin_theta_h * cos_phi_h, sin_theta_h * sin_phi_h, cos_theta_h);
@@ -511,9 +512,9 @@ static v3 SampleGTR2(float xi_1, float xi_2, v3 V, v3 N, float alpha) {
 /* SampleGTR1 IS:519-536 */
 static v3 SampleGTR1(float xi_1, float xi_2, v3 V, v3 N, float alpha) {
   float phi_h = 2.0f * PI * xi_1;
-  float sin_phi_h = sinf(phi_h);
-  float cos_phi_h = cosf(phi_h);
-  float cos_theta_h = sqrtf((1.0f - powf(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));
+  float sin_phi_h = ptm_sinf(phi_h);
+  float cos_phi_h = ptm_cosf(phi_h);
+  float cos_theta_h = sqrtf((1.0f - ptm_powf(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));
   float sin_theta_h = sqrtf(fmaxf(0.0f, 1.0f - cos_theta_h * cos_theta_h));
   v3 H = V3(sin_theta_h * cos_phi_h, sin_theta_h * sin_phi_h, cos_theta_h);
   H = toNormalHemisphere(H, N);

@@ -1,0 +1,113 @@
+"""Integer parity of the random streams (bit-exact): wang hash (pass1.fsh:78-85),
+the per-pixel seed (:73-76), rand() (:87-89), the verbatim Sobol table (:92-94)
+pinned against the published Joe-Kuo construction, grayCode, sobol() (:101-109)
+and the Cranley-Patterson shift (:118-136)."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle
+
+ROOT = Path(__file__).resolve().parent.parent
+M32 = 0xFFFFFFFF
+
+
+def wang_py(s):
+    """pass1.fsh:78-85 restated in Python integers."""
+    s = ((s ^ 61) ^ (s >> 16)) & M32
+    s = (s * 9) & M32
+    s = s ^ (s >> 4)
+    s = (s * 0x27D4EB2D) & M32
+    s = s ^ (s >> 15)
+    return s
+
+
+def table(path):
+    src = Path(path).read_text()
+    i = src.index("[8 * 32]")
+    return [int(x) for x in re.findall(r"(\d+)u", src[i:src.index("};", i)])]
+
+
+# Joe & Kuo (2008) new-joe-kuo-6.21201 parameters of dimensions 2..9: (s, a, m_1..m_s)
+JOE_KUO = {2: (1, 0, [1]), 3: (2, 1, [1, 3]), 4: (3, 1, [1, 3, 1]), 5: (3, 2, [1, 1, 1]), 6: (4, 1, [1, 1, 3, 3]),
+           7: (4, 4, [1, 3, 5, 13]), 8: (5, 2, [1, 1, 5, 5, 17]), 9: (5, 4, [1, 1, 5, 5, 5])}
+
+
+def joe_kuo(d):
+    if d == 1:
+        return [1 << (32 - i) for i in range(1, 33)]
+    s, a, m = JOE_KUO[d]
+    V = [0] * 33
+    for i in range(1, s + 1):
+        V[i] = m[i - 1] << (32 - i)
+    for i in range(s + 1, 33):
+        V[i] = V[i - s] ^ (V[i - s] >> s)
+        for k in range(1, s):
+            V[i] ^= ((a >> (s - 1 - k)) & 1) * V[i - k]
+    return V[1:]
+
+
+def test_wang_hash_matches_restatement():
+    rng = np.random.default_rng(0)
+    for s in list(rng.integers(0, 2 ** 32, 2000, dtype=np.uint64)) + [0, 1, 61, M32, 0x80000000]:
+        assert oracle.wang_hash(int(s)) == wang_py(int(s))
+
+
+def test_pixel_rng_stream():
+    for (px, py, f) in [(0, 0, 0), (17, 5, 3), (1919, 1079, 100000)]:
+        seed = ((px * 1973 + py * 9277 + f * 26699) & M32) | 1
+        want = []
+        for _ in range(8):
+            seed = wang_py(seed)
+            want.append(np.float32(seed) / np.float32(4294967296.0))
+        got = oracle.pixel_rng(px, py, f, 8)
+        assert np.array_equal(got, np.array(want, np.float32))
+        assert np.all((got >= 0) & (got <= 1))
+
+
+def test_sobol_table_is_joe_kuo_except_dims_5_and_7():
+    tab = table(ROOT / "oracle" / "pt_oracle.c")
+    assert len(tab) == 256
+    for dim, jk in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (6, 7)]:
+        assert tab[32 * dim:32 * dim + 32] == joe_kuo(jk), dim
+    for dim in (5, 7):  # non-standard in the reference: used verbatim
+        row = tab[32 * dim:32 * dim + 32]
+        assert all(row != joe_kuo(d) for d in range(1, 10))
+        assert row[0] == 1 << 31
+
+
+def test_device_table_equals_oracle_table():
+    a = table(ROOT / "oracle" / "pt_oracle.c")
+    b = table(ROOT / "opengl_ray_tracing_amd" / "csrc" / "pt_kernels.hip")
+    assert a == b
+
+
+def sobol_py(tab, d, i):
+    r = 0
+    off = (d & 7) * 32
+    j = 0
+    while i:
+        if i & 1:
+            r ^= tab[off + j]
+        i >>= 1
+        j += 1
+    if d >= 8:
+        r ^= wang_py(d)
+    return np.float32(r) * (np.float32(1.0) / np.float32(4294967295.0))
+
+
+@pytest.mark.parametrize("d", range(0, 12))
+def test_sobol_values(d):
+    tab = table(ROOT / "oracle" / "pt_oracle.c")
+    for frame in [0, 1, 2, 7, 100, 65535, 10 ** 6]:
+        i = frame + 1
+        g = i ^ (i >> 1)  # grayCode
+        assert oracle.sobol(d, g) == sobol_py(tab, d, g)
+
+
+def test_sobol_dim0_is_van_der_corput():
+    # dim 0 with gray-code index visits the dyadic points of [0,1) once per 2^k frames
+    pts = sorted(oracle.sobol(0, (i ^ (i >> 1))) for i in range(0, 64))
+    assert np.allclose(np.diff(pts), 1 / 64, atol=1e-7)
