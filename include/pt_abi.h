@@ -48,6 +48,7 @@ extern "C" {
 #define PT_FLAG_NO_CULL 0x1u      /* traverse exactly like pass1.fsh:335-382 (no closest-t culling) */
 #define PT_FLAG_CLOSEST_SHADOW 0x2u /* env shadow rays use closest-hit instead of any-hit */
 #define PT_FLAG_COUNT_FETCHES 0x4u /* count reference-algorithm fetches (implies NO_CULL, closest shadow) */
+#define PT_FLAG_WAVEFRONT 0x8u    /* staged wavefront pipeline instead of the persistent megakernel */
 
 typedef struct pt_config {
   int width;          /* RenderPass::width  (OpenglRayTracing/main.cpp:83), e.g. 1920 */

@@ -35,9 +35,12 @@ CXX_FLAGS = ["-O2", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-fast-math"
              "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"]
 
 SOURCES = {
-    "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h",
+    "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h", CSRC / "pt_trace.h",
                                                        INCLUDE / "pt_fmath.h"]),
-    "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
+    "pt_wavefront.o": ("hip", CSRC / "pt_wavefront.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h",
+                                                           CSRC / "pt_trace.h", CSRC / "pt_wavefront.h",
+                                                           INCLUDE / "pt_fmath.h"]),
+    "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", CSRC / "pt_wavefront.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
                                                        INCLUDE / "pt_fmath.h"]),
     "scene.o": ("cxx", CSRC / "scene.cpp", [INCLUDE / "pt_scene.h"]),
 }
@@ -79,6 +82,33 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
     if force or jobs or _stale(LIB, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)])
     return LIB
+
+
+VARIANTS = PKG / "_variants"
+
+
+def variant_lib(name: str) -> Path:
+    return VARIANTS / f"libpt_{name}.so"
+
+
+def build_variant(name: str, defines: dict) -> Path:
+    """A tuning build of libpt.so with extra -D defines (e.g. PT_MIN_WAVES, PT_LDS_STACK),
+    kept in-tree under _variants/ so tools/tune.py can A/B it on the GPU box."""
+    out_dir = VARIANTS / name
+    out_dir.mkdir(parents=True, exist_ok=True)
+    dflags = [f"-D{k}={v}" for k, v in defines.items()]
+    inc = [f"-I{INCLUDE}", f"-I{CSRC}"]
+    objs = []
+    for obj, (kind, src, deps) in SOURCES.items():
+        out = out_dir / obj
+        objs.append(out)
+        if kind == "hip":
+            _run([HIPCC, *HIP_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
+        else:
+            _run(["g++", *CXX_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
+    lib = variant_lib(name)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(lib), *map(str, objs)])
+    return lib
 
 
 def build_oracle(force: bool = False) -> Path:

@@ -92,8 +92,23 @@ SIGNATURES = {
 }
 
 
+_variant = None
+
+
+def use_variant(name: str | None) -> None:
+    """Select an in-tree tuning build (``_build.build_variant(name, ...)``) before the first
+    load; used by tools/tune.py for A/B measurements. Names are restricted to [A-Za-z0-9_]."""
+    import re
+    global _variant
+    if _lib is not None:
+        raise RuntimeError("use_variant() must be called before the library is loaded")
+    if name is not None and not re.fullmatch(r"[A-Za-z0-9_]{1,32}", name):
+        raise ValueError(f"bad variant name {name!r}")
+    _variant = name
+
+
 def lib_path() -> Path:
-    return _build.LIB
+    return _build.variant_lib(_variant) if _variant else _build.LIB
 
 
 def load(build_if_missing: bool = False):

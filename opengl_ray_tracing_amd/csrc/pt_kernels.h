@@ -7,7 +7,13 @@
 namespace pt {
 
 constexpr int BLOCK = 256;        // 4 waves of 64
-constexpr int LDS_STACK = 32;     // traversal stack entries per lane kept in LDS (32 KiB per block)
+#ifndef PT_LDS_STACK
+#define PT_LDS_STACK 32
+#endif
+#ifndef PT_MIN_WAVES
+#define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
+#endif
+constexpr int LDS_STACK = PT_LDS_STACK;  // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
 constexpr int NUM_QUEUES = 8;     // work counters, one per blockIdx % 8 group (XCD round-robin)
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;

@@ -22,174 +22,11 @@
 
 #include "pt_device.h"
 #include "pt_kernels.h"
+#include "pt_trace.h"
 
 namespace pt {
 
-__constant__ uint32_t kSobolV[8 * 32] = {
-    2147483648u,1073741824u,536870912u,268435456u,134217728u,67108864u,33554432u,16777216u,8388608u,4194304u,2097152u,1048576u,524288u,262144u,131072u,65536u,32768u,16384u,8192u,4096u,2048u,1024u,512u,256u,128u,64u,32u,16u,8u,4u,2u,1u,
-    2147483648u,3221225472u,2684354560u,4026531840u,2281701376u,3422552064u,2852126720u,4278190080u,2155872256u,3233808384u,2694840320u,4042260480u,2290614272u,3435921408u,2863267840u,4294901760u,2147516416u,3221274624u,2684395520u,4026593280u,2281736192u,3422604288u,2852170240u,4278255360u,2155905152u,3233857728u,2694881440u,4042322160u,2290649224u,3435973836u,2863311530u,4294967295u,
-    2147483648u,3221225472u,1610612736u,2415919104u,3892314112u,1543503872u,2382364672u,3305111552u,1753219072u,2629828608u,3999268864u,1435500544u,2154299392u,3231449088u,1626210304u,2421489664u,3900735488u,1556135936u,2388680704u,3314585600u,1751705600u,2627492864u,4008611328u,1431684352u,2147543168u,3221249216u,1610649184u,2415969680u,3892340840u,1543543964u,2382425838u,3305133397u,
-    2147483648u,3221225472u,536870912u,1342177280u,4160749568u,1946157056u,2717908992u,2466250752u,3632267264u,624951296u,1507852288u,3872391168u,2013790208u,3020685312u,2181169152u,3271884800u,546275328u,1363623936u,4226424832u,1977167872u,2693105664u,2437829632u,3689389568u,635137280u,1484783744u,3846176960u,2044723232u,3067084880u,2148008184u,3222012020u,537002146u,1342505107u,
-    2147483648u,1073741824u,536870912u,2952790016u,4160749568u,3690987520u,2046820352u,2634022912u,1518338048u,801112064u,2707423232u,4038066176u,3666345984u,1875116032u,2170683392u,1085997056u,579305472u,3016343552u,4217741312u,3719483392u,2013407232u,2617981952u,1510979072u,755882752u,2726789248u,4090085440u,3680870432u,1840435376u,2147625208u,1074478300u,537900666u,2953698205u,
-    2147483648u,1073741824u,1610612736u,805306368u,2818572288u,335544320u,2113929216u,3472883712u,2290089984u,3829399552u,3059744768u,1127219200u,3089629184u,4199809024u,3567124480u,1891565568u,394297344u,3988799488u,920674304u,4193267712u,2950604800u,3977188352u,3250028032u,129093376u,2231568512u,2963678272u,4281226848u,432124720u,803643432u,1633613396u,2672665246u,3170194367u,
-    2147483648u,3221225472u,2684354560u,3489660928u,1476395008u,2483027968u,1040187392u,3808428032u,3196059648u,599785472u,505413632u,4077912064u,1182269440u,1736704000u,2017853440u,2221342720u,3329785856u,2810494976u,3628507136u,1416089600u,2658719744u,864310272u,3863387648u,3076993792u,553150080u,272922560u,4167467040u,1148698640u,1719673080u,2009075780u,2149644390u,3222291575u,
-    2147483648u,1073741824u,2684354560u,1342177280u,2281701376u,1946157056u,436207616u,2566914048u,2625634304u,3208642560u,2720006144u,2098200576u,111673344u,2354315264u,3464626176u,4027383808u,2886631424u,3770826752u,1691164672u,3357462528u,1993345024u,3752330240u,873073152u,2870150400u,1700563072u,87021376u,1097028000u,1222351248u,1560027592u,2977959924u,23268898u,437609937u};
 
-// ----------------------------------------------------------------- counters
-struct Counters {
-  uint32_t rays, nodes, tris, mats, texels;
-};
-
-// ----------------------------------------------------------------- stack
-// LDS stack of LDS_STACK entries per lane, entry e of thread t at
-// lds[(e % LDS_STACK) * BLOCK + t]; entries older than the newest LDS_STACK
-// live in the thread's HBM overflow region gbl[e] (only when the tree is
-// deeper than LDS_STACK).
-struct Stack {
-  int* lds;   // &s_stack[threadIdx.x]
-  int* gbl;   // overflow region (may be null when maxStack <= LDS_STACK)
-  int sp;
-  __device__ __forceinline__ void push(int v) {
-    int slot = sp & (LDS_STACK - 1);
-    if (sp >= LDS_STACK) gbl[sp - LDS_STACK] = lds[slot * BLOCK];
-    lds[slot * BLOCK] = v;
-    sp++;
-  }
-  __device__ __forceinline__ int pop() {
-    sp--;
-    int slot = sp & (LDS_STACK - 1);
-    int v = lds[slot * BLOCK];
-    if (sp >= LDS_STACK) lds[slot * BLOCK] = gbl[sp - LDS_STACK];
-    return v;
-  }
-};
-
-// hitAABB IS:303-316 with the precomputed reciprocal direction (the reference
-// recomputes the same 1/d per box). Returns the reference's d; t0 (the slab
-// entry) is returned for culling.
-__device__ __forceinline__ float hitAABB(V3 o, V3 inv, float4 lo, float4 hi, float& t0out) {
-  float fx = (hi.x - o.x) * inv.x, fy = (hi.y - o.y) * inv.y, fz = (hi.z - o.z) * inv.z;
-  float nx = (lo.x - o.x) * inv.x, ny = (lo.y - o.y) * inv.y, nz = (lo.z - o.z) * inv.z;
-  float t1 = fminf(fmaxf(fx, nx), fminf(fmaxf(fy, ny), fmaxf(fz, nz)));
-  float t0 = fmaxf(fminf(fx, nx), fmaxf(fminf(fy, ny), fminf(fz, nz)));
-  t0out = t0;
-  return (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
-}
-
-// hitTriangle IS:251-301, accept/reject and distance only. With the stored unit
-// normal Ng = normalize(cross(p2-p1,p3-p1)) and w = dot(Ng,p1) (computed on the
-// host in the reference's order) this rounds exactly like the reference: the
-// orientation flip negates numerator, denominator and all three edge tests
-// exactly, so it changes neither t nor the accept decision.
-__device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float& t) {
-  float4 A = g[0], B = g[1], C = g[2], Nn = g[3];
-  V3 N = v3(Nn.x, Nn.y, Nn.z);
-  float dn = dot(N, d);
-  if (fabsf(dn) < 0.00001f) return false;
-  float tt = (A.w - dot(o, N)) / dn;
-  if (tt < 0.0005f) return false;
-  V3 p1 = v3(A.x, A.y, A.z), p2 = v3(B.x, B.y, B.z), p3 = v3(C.x, C.y, C.z);
-  V3 P = o + d * tt;
-  float s1 = dot(cross(p2 - p1, P - p1), N);
-  float s2 = dot(cross(p3 - p2, P - p2), N);
-  float s3 = dot(cross(p1 - p3, P - p3), N);
-  bool r1 = (s1 > 0 && s2 > 0 && s3 > 0);
-  bool r2 = (s1 < 0 && s2 < 0 && s3 < 0);
-  t = tt;
-  return r1 || r2;
-}
-
-// hitBVH IS:335-382: same visiting order (nearer child by the reference's d
-// first, ties to the right child), strict '<' closest update, so the same
-// triangle wins. CULL skips children whose slab entry lies beyond the current
-// closest hit (plus a margin); ANYHIT returns on the first accepted triangle
-// (used for env shadow rays, where only isHit is read: IS:776-779).
-template <bool ANYHIT, bool CULL, bool COUNT>
-__device__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, Stack& st, Counters& C) {
-  V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  float tbest = PT_INF;
-  int best = -1;
-  int ref = S.rootRef;
-  st.sp = 0;
-  C.rays++;
-  while (true) {
-    if (ref >= 0) {
-      const float4* nd = S.bvh + 4 * (size_t)ref;
-      float4 la = nd[0], lb = nd[1], ra = nd[2], rb = nd[3];
-      int lref = __float_as_int(la.w), rref = __float_as_int(lb.w);
-      float t0l, t0r;
-      float d1 = hitAABB(o, inv, la, lb, t0l);
-      float d2 = hitAABB(o, inv, ra, rb, t0r);
-      bool h1 = (lref != REF_NONE) && d1 > 0.0f;
-      bool h2 = (rref != REF_NONE) && d2 > 0.0f;
-      if (COUNT) C.nodes += 1u + (lref != REF_NONE) + (rref != REF_NONE);
-      if (CULL) {
-        float lim = tbest + 1e-3f * fmaxf(1.0f, tbest);
-        h1 = h1 && !(t0l > lim);
-        h2 = h2 && !(t0r > lim);
-      }
-      if (h1 && h2) {
-        bool leftFirst = d1 < d2;
-        st.push(leftFirst ? rref : lref);
-        ref = leftFirst ? lref : rref;
-        continue;
-      }
-      if (h1) { ref = lref; continue; }
-      if (h2) { ref = rref; continue; }
-    } else if (ref != REF_NONE) {
-      uint32_t v = ~(uint32_t)ref;
-      int start = (int)(v >> LEAF_CNT_BITS);
-      int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
-      if (COUNT) C.nodes++;
-      float localBest = PT_INF;
-      for (int k = 0; k < cnt; k++) {
-        int i = start + k;
-        float t;
-        bool hit = triHit(S.geo + 4 * (size_t)i, o, d, t);
-        if (COUNT) {
-          C.tris++;
-          if (hit && t < localBest) { localBest = t; C.mats++; }
-        }
-        if (hit && t < tbest) {
-          tbest = t;
-          best = i;
-          if (ANYHIT) { tOut = tbest; return best; }
-        }
-      }
-    }
-    if (st.sp == 0) break;
-    ref = st.pop();
-  }
-  tOut = tbest;
-  return best;
-}
-
-// The full HitResult (IS:63-71) of the winning triangle, computed once.
-struct Hit {
-  V3 P, N, viewDir;
-  Material m;
-};
-__device__ __forceinline__ void finishHit(const SceneView& S, int tri, V3 o, V3 d, float t, Hit& h) {
-  const float4* g = S.geo + 4 * (size_t)tri;
-  float4 A = g[0], B = g[1], C4 = g[2], Nn = g[3];
-  V3 p1 = v3(A.x, A.y, A.z), p2 = v3(B.x, B.y, B.z), p3 = v3(C4.x, C4.y, C4.z);
-  bool inside = dot(v3(Nn.x, Nn.y, Nn.z), d) > 0.0f;
-  V3 P = o + d * t;
-  float alpha = (-(P.x - p2.x) * (p3.y - p2.y) + (P.y - p2.y) * (p3.x - p2.x)) /
-                (-(p1.x - p2.x - 0.00005f) * (p3.y - p2.y + 0.00005f) + (p1.y - p2.y + 0.00005f) * (p3.x - p2.x + 0.00005f));
-  float beta = (-(P.x - p3.x) * (p1.y - p3.y) + (P.y - p3.y) * (p1.x - p3.x)) /
-               (-(p2.x - p3.x - 0.00005f) * (p1.y - p3.y + 0.00005f) + (p2.y - p3.y + 0.00005f) * (p1.x - p3.x + 0.00005f));
-  float gama = 1.0f - alpha - beta;
-  const float* rec = S.attr + 36 * (size_t)tri;
-  const float4* q = reinterpret_cast<const float4*>(rec + 8);
-  float4 q0 = q[0], q1 = q[1], q2 = q[2];  // floats 8..19
-  V3 n1 = v3(q0.y, q0.z, q0.w), n2 = v3(q1.x, q1.y, q1.z), n3 = v3(q1.w, q2.x, q2.y);
-  V3 Ns = normalize((n1 * alpha + n2 * beta) + n3 * gama);
-  h.P = P;
-  h.N = inside ? -Ns : Ns;
-  h.viewDir = d;
-  h.m = loadMaterial(rec);
-}
 
 // ------------------------------------------------------------ integrators
 template <bool CULL, bool COUNT>
@@ -503,7 +340,7 @@ __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
 }
 
 template <int INTEG, bool CULL, bool COUNT>
-__global__ __launch_bounds__(BLOCK) void renderKernel(RenderParams p) {
+__global__ __launch_bounds__(BLOCK, PT_MIN_WAVES) void renderKernel(RenderParams p) {
   __shared__ int s_stack[LDS_STACK * BLOCK];
   Stack st;
   st.lds = s_stack + threadIdx.x;

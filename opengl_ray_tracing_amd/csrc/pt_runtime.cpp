@@ -18,8 +18,12 @@
 #include "pt_fmath.h"
 #include "pt_kernels.h"
 #include "pt_scene.h"
+#include "pt_wavefront.h"
 
 using namespace pt;
+
+static constexpr size_t CTL_RAY_SHARDS = 512;
+static constexpr size_t CTL_BYTES = CTL_RAY_SHARDS + WF_NSEG * sizeof(unsigned long long);
 
 struct pt_ctx {
   pt_config cfg{};
@@ -43,7 +47,9 @@ struct pt_ctx {
   int nShapes = 0;
   // frame state
   float4* d_accum = nullptr;
-  unsigned char* d_ctl = nullptr;  // [0,32) queue counters (zeroed per launch), [64,104) cumulative stats
+  // [0,32) queue counters (zeroed per launch), [64,104) cumulative stats,
+  // [CTL_RAY_SHARDS, CTL_BYTES) WF_NSEG sharded cumulative ray counters
+  unsigned char* d_ctl = nullptr;
   int* d_ovf = nullptr;
   size_t ovfInts = 0;
   // shards
@@ -54,6 +60,10 @@ struct pt_ctx {
   int* d_tri = nullptr;
   size_t traceCap = 0;
   float* d_rgb = nullptr;
+  // wavefront pipeline state (allocated on first use)
+  WFState wf{};
+  WFQueues wfq{};
+  bool wfReady = false;
 };
 
 static std::string g_create_err;
@@ -79,6 +89,8 @@ static void dfree(T*& p) {
 }
 
 extern "C" {
+
+static void freeWavefront(pt_ctx* ctx);
 
 int pt_device_count(int* n) {
   if (!n) return PT_E_INVALID;
@@ -141,8 +153,8 @@ int pt_create(pt_ctx** out, const pt_config* cfg) {
   const size_t npix = (size_t)cfg->width * cfg->height;
   CKC(hipMalloc(&ctx->d_accum, npix * sizeof(float4)));
   CKC(hipMemset(ctx->d_accum, 0, npix * sizeof(float4)));
-  CKC(hipMalloc(&ctx->d_ctl, 128));
-  CKC(hipMemset(ctx->d_ctl, 0, 128));
+  CKC(hipMalloc(&ctx->d_ctl, CTL_BYTES));
+  CKC(hipMemset(ctx->d_ctl, 0, CTL_BYTES));
   ctx->shardsX = (cfg->width + ss - 1) / ss;
   ctx->shardsY = (cfg->height + ss - 1) / ss;
   const int numShards = ctx->shardsX * ctx->shardsY;
@@ -162,6 +174,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
+  freeWavefront(ctx);
   for (hipEvent_t e : ctx->evs) (void)hipEventDestroy(e);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
@@ -339,9 +352,9 @@ static SceneView sceneView(const pt_ctx* ctx) {
   return s;
 }
 
-// make sure the overflow stack covers `threads` threads
-static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth) {
-  *ovfDepth = ctx->maxStack > LDS_STACK ? ctx->maxStack - LDS_STACK + 1 : 0;
+// make sure the overflow stack covers `threads` threads of a kernel keeping `ldsDepth` entries in LDS
+static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDepth = LDS_STACK) {
+  *ovfDepth = ctx->maxStack > ldsDepth ? ctx->maxStack - ldsDepth + 1 : 0;
   if (*ovfDepth == 0) return PT_OK;
   size_t need = threads * (size_t)(*ovfDepth);
   if (need > ctx->ovfInts) {
@@ -349,6 +362,121 @@ static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth) {
     CK(hipMalloc(&ctx->d_ovf, need * sizeof(int)));
     ctx->ovfInts = need;
   }
+  return PT_OK;
+}
+
+// ------------------------------------------------------------ wavefront pipeline
+static int ensureWavefront(pt_ctx* ctx) {
+  if (ctx->wfReady) return PT_OK;
+  const size_t n = (size_t)ctx->cfg.width * ctx->cfg.height;
+  WFState& s = ctx->wf;
+  CK(hipMalloc(&s.rayO, n * sizeof(float4)));
+  CK(hipMalloc(&s.rayD, n * sizeof(float4)));
+  CK(hipMalloc(&s.shD, n * sizeof(float4)));
+  CK(hipMalloc(&s.hit, n * sizeof(int2)));
+  CK(hipMalloc(&s.occ, n * sizeof(int)));
+  CK(hipMalloc(&s.seed, n * sizeof(uint32_t)));
+  CK(hipMalloc(&s.flags, n * sizeof(uint32_t)));
+  CK(hipMalloc(&s.hist, n * sizeof(float4)));
+  CK(hipMalloc(&s.Lo, n * sizeof(float4)));
+  CK(hipMalloc(&s.Le0, n * sizeof(float4)));
+  CK(hipMalloc(&s.pend, n * sizeof(float4)));
+  CK(hipMalloc(&s.shC, n * sizeof(float4)));
+  // segment s of a queue holds the wave tiles s, s+WF_NSEG, ... of the frame
+  const size_t tiles = (size_t)ctx->numItems;
+  ctx->wfq.segCap = (int)(((tiles + WF_NSEG - 1) / WF_NSEG) * 64);
+  const size_t qn = (size_t)WF_NSEG * ctx->wfq.segCap;
+  for (int k = 0; k < 2; k++) {
+    CK(hipMalloc(&ctx->wfq.act[k], qn * sizeof(int)));
+    CK(hipMalloc(&ctx->wfq.cls[k], qn * sizeof(int)));
+    CK(hipMalloc(&ctx->wfq.shd[k], qn * sizeof(int)));
+  }
+  CK(hipMalloc(&ctx->wfq.cnt, (size_t)wfCnt(256, 0) * sizeof(int)));
+  ctx->wfReady = true;
+  return PT_OK;
+}
+
+static void freeWavefront(pt_ctx* ctx) {
+  WFState& s = ctx->wf;
+  dfree(s.rayO); dfree(s.rayD); dfree(s.shD); dfree(s.hit); dfree(s.occ); dfree(s.seed);
+  dfree(s.flags); dfree(s.hist); dfree(s.Lo); dfree(s.Le0); dfree(s.pend); dfree(s.shC);
+  for (int k = 0; k < 2; k++) {
+    dfree(ctx->wfq.act[k]); dfree(ctx->wfq.cls[k]); dfree(ctx->wfq.shd[k]);
+  }
+  dfree(ctx->wfq.cnt);
+  ctx->wfReady = false;
+}
+
+// gen -> [trace closest (+ shadow) -> shade] x (maxBounce + 1), all on ctx->stream
+static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16], uint32_t frameCounter, bool cull,
+                           unsigned long long* stats, hipEvent_t evb, hipEvent_t eve) {
+  const pt_config& c = ctx->cfg;
+  (void)stats;
+  unsigned long long* rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAY_SHARDS);
+  int rc = ensureWavefront(ctx);
+  if (rc) return rc;
+  const int maxBounce = c.max_bounce >= 0 ? c.max_bounce : defaultBounce(c.integrator);
+  if (maxBounce > 250) return fail(ctx, PT_E_INVALID, "max_bounce too large for the wavefront pipeline");
+  const bool mis = c.integrator == PT_DISNEY_MIS_SOBOL_IS;
+  int nbC = 0, nbS = 0;
+  CK(wfTraceBlocksPerCU(false, cull, &nbC));
+  CK(wfTraceBlocksPerCU(true, cull, &nbS));
+  // consumer blocks own segment blockIdx % WF_NSEG: grids are multiples of WF_NSEG
+  auto segGrid = [](long g) { return (int)std::max<long>(WF_NSEG, (g + WF_NSEG - 1) / WF_NSEG * WF_NSEG); };
+  const int gridC = segGrid((long)ctx->numCU * std::max(nbC, 1)), gridS = segGrid((long)ctx->numCU * std::max(nbS, 1));
+  int ovfDepth = 0;
+  rc = ensureOverflow(ctx, (size_t)std::max(gridC, gridS) * BLOCK, &ovfDepth, WF_LDS_STACK);
+  if (rc) return rc;
+  WFParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.scene = sceneView(ctx);
+  p.env.hdr = ctx->d_hdr;
+  p.env.cache = ctx->d_cache;
+  p.env.w = ctx->hdrW;
+  p.env.h = ctx->hdrH;
+  p.env.res = ctx->hdrW;
+  p.st = ctx->wf;
+  p.q = ctx->wfq;
+  p.accum = ctx->d_accum;
+  p.width = c.width;
+  p.height = c.height;
+  p.frameCounter = frameCounter;
+  p.maxBounce = maxBounce;
+  std::memcpy(p.eye, eye, sizeof(p.eye));
+  std::memcpy(p.cam, cam, sizeof(p.cam));
+  p.numOwned = ctx->numItems * 64;
+  p.shardSize = ctx->shardSize;
+  p.shardsX = ctx->shardsX;
+  p.rank = c.tile_rank;
+  p.world = c.tile_world;
+  CK(hipMemsetAsync(ctx->wfq.cnt, 0, (size_t)wfCnt(maxBounce + 2, 0) * sizeof(int), ctx->stream));
+  const int gridShade = segGrid(std::min<long>(((long)p.numOwned + BLOCK - 1) / BLOCK, (long)ctx->numCU * 16));
+  CK(hipEventRecord(evb, ctx->stream));
+  CK(wfLaunchGen(p, ctx->stream));
+  for (int s = 0; s <= maxBounce; s++) {
+    WFTraceParams t;
+    t.scene = p.scene;
+    t.ovf = ovfDepth ? ctx->d_ovf : nullptr;
+    t.ovfDepth = ovfDepth;
+    t.rays = rayShards;
+    t.rayO = ctx->wf.rayO;
+    t.segCap = ctx->wfq.segCap;
+    t.queue = ctx->wfq.cls[s & 1];
+    t.count = ctx->wfq.cnt + wfCnt(s, WF_CNT_CLS);
+    t.rayD = ctx->wf.rayD;
+    t.hit = ctx->wf.hit;
+    t.occ = ctx->wf.occ;
+    CK(wfLaunchTrace(t, false, cull, gridC, ctx->stream));
+    if (mis && s > 0) {
+      t.queue = ctx->wfq.shd[s & 1];
+      t.count = ctx->wfq.cnt + wfCnt(s, WF_CNT_SHD);
+      t.rayD = ctx->wf.shD;
+      CK(wfLaunchTrace(t, true, cull, gridS, ctx->stream));
+    }
+    CK(wfLaunchShade(p, c.integrator, s, gridShade, ctx->stream));
+  }
+  CK(hipEventRecord(eve, ctx->stream));
+  ctx->launches++;
   return PT_OK;
 }
 
@@ -383,6 +511,8 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   if (!ctx->d_bvh || !eye || !cameraRotate) return fail(ctx, ctx->d_bvh ? PT_E_INVALID : PT_E_NOSCENE, "no scene");
   const bool count = (c.flags & PT_FLAG_COUNT_FETCHES) != 0;
   const bool cull = !count && !(c.flags & PT_FLAG_NO_CULL);
+  if (!count && (c.flags & PT_FLAG_WAVEFRONT))
+    return renderWavefront(ctx, eye, cameraRotate, frameCounter, cull, stats, evb, eve);
   int nb = 0;
   CK(renderBlocksPerCU(c.integrator, cull, count, &nb));
   if (nb < 1) nb = 1;
@@ -559,10 +689,12 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   if (!ctx || !st) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
-  unsigned long long h[5];
+  unsigned long long h[5], shards[WF_NSEG];
   CK(hipMemcpy(h, ctx->d_ctl + 64, sizeof(h), hipMemcpyDeviceToHost));
+  CK(hipMemcpy(shards, ctx->d_ctl + CTL_RAY_SHARDS, sizeof(shards), hipMemcpyDeviceToHost));
   std::memset(st, 0, sizeof(*st));
   st->rays = h[0];
+  for (int k = 0; k < WF_NSEG; k++) st->rays += shards[k];
   st->node_fetch = h[1];
   st->tri_fetch = h[2];
   st->mat_fetch = h[3];
@@ -623,7 +755,7 @@ int pt_reset_stats(pt_ctx* ctx) {
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
-  CK(hipMemset(ctx->d_ctl + 64, 0, 64));
+  CK(hipMemset(ctx->d_ctl + 64, 0, CTL_BYTES - 64));
   ctx->launches = 0;
   return PT_OK;
 }

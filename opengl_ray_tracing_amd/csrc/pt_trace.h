@@ -1,0 +1,171 @@
+// pt_trace.h -- BVH traversal and triangle intersection shared by the
+// megakernel (pt_kernels.hip) and the wavefront trace kernels
+// (pt_wavefront.hip). Restates hitBVH / hitArray / hitTriangle / hitAABB of
+// ImportanceSampling_LowDiscrepancySequence/shaders/pass1.fsh:251-382 over the
+// re-laid-out device scene (pt_kernels.h SceneView).
+#pragma once
+#include "pt_device.h"
+#include "pt_kernels.h"
+
+namespace pt {
+
+// ----------------------------------------------------------------- counters
+struct Counters {
+  uint32_t rays, nodes, tris, mats, texels;
+};
+
+// ----------------------------------------------------------------- stack
+// LDS stack of LDS_STACK entries per lane, entry e of thread t at
+// lds[(e % LDS_STACK) * BLOCK + t]; entries older than the newest LDS_STACK
+// live in the thread's HBM overflow region gbl[e] (only when the tree is
+// deeper than LDS_STACK).
+template <int DEPTH, int STRIDE>
+struct StackT {
+  static_assert((DEPTH & (DEPTH - 1)) == 0, "LDS stack depth must be a power of two");
+  int* lds;   // &s_stack[threadIdx.x]
+  int* gbl;   // overflow region (may be null when maxStack <= DEPTH)
+  int sp;
+  __device__ __forceinline__ void push(int v) {
+    int slot = sp & (DEPTH - 1);
+    if (sp >= DEPTH) gbl[sp - DEPTH] = lds[slot * STRIDE];
+    lds[slot * STRIDE] = v;
+    sp++;
+  }
+  __device__ __forceinline__ int pop() {
+    sp--;
+    int slot = sp & (DEPTH - 1);
+    int v = lds[slot * STRIDE];
+    if (sp >= DEPTH) lds[slot * STRIDE] = gbl[sp - DEPTH];
+    return v;
+  }
+};
+using Stack = StackT<LDS_STACK, BLOCK>;
+
+// hitAABB IS:303-316 with the precomputed reciprocal direction (the reference
+// recomputes the same 1/d per box). Returns the reference's d; t0 (the slab
+// entry) is returned for culling.
+__device__ __forceinline__ float hitAABB(V3 o, V3 inv, float4 lo, float4 hi, float& t0out) {
+  float fx = (hi.x - o.x) * inv.x, fy = (hi.y - o.y) * inv.y, fz = (hi.z - o.z) * inv.z;
+  float nx = (lo.x - o.x) * inv.x, ny = (lo.y - o.y) * inv.y, nz = (lo.z - o.z) * inv.z;
+  float t1 = fminf(fmaxf(fx, nx), fminf(fmaxf(fy, ny), fmaxf(fz, nz)));
+  float t0 = fmaxf(fminf(fx, nx), fmaxf(fminf(fy, ny), fminf(fz, nz)));
+  t0out = t0;
+  return (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
+}
+
+// hitTriangle IS:251-301, accept/reject and distance only. With the stored unit
+// normal Ng = normalize(cross(p2-p1,p3-p1)) and w = dot(Ng,p1) (computed on the
+// host in the reference's order) this rounds exactly like the reference: the
+// orientation flip negates numerator, denominator and all three edge tests
+// exactly, so it changes neither t nor the accept decision.
+__device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float& t) {
+  float4 A = g[0], B = g[1], C = g[2], Nn = g[3];
+  V3 N = v3(Nn.x, Nn.y, Nn.z);
+  float dn = dot(N, d);
+  if (fabsf(dn) < 0.00001f) return false;
+  float tt = (A.w - dot(o, N)) / dn;
+  if (tt < 0.0005f) return false;
+  V3 p1 = v3(A.x, A.y, A.z), p2 = v3(B.x, B.y, B.z), p3 = v3(C.x, C.y, C.z);
+  V3 P = o + d * tt;
+  float s1 = dot(cross(p2 - p1, P - p1), N);
+  float s2 = dot(cross(p3 - p2, P - p2), N);
+  float s3 = dot(cross(p1 - p3, P - p3), N);
+  bool r1 = (s1 > 0 && s2 > 0 && s3 > 0);
+  bool r2 = (s1 < 0 && s2 < 0 && s3 < 0);
+  t = tt;
+  return r1 || r2;
+}
+
+// hitBVH IS:335-382: same visiting order (nearer child by the reference's d
+// first, ties to the right child), strict '<' closest update, so the same
+// triangle wins. CULL skips children whose slab entry lies beyond the current
+// closest hit (plus a margin); ANYHIT returns on the first accepted triangle
+// (used for env shadow rays, where only isHit is read: IS:776-779).
+template <bool ANYHIT, bool CULL, bool COUNT, class StackType>
+__device__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C) {
+  V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  float tbest = PT_INF;
+  int best = -1;
+  int ref = S.rootRef;
+  st.sp = 0;
+  C.rays++;
+  while (true) {
+    if (ref >= 0) {
+      const float4* nd = S.bvh + 4 * (size_t)ref;
+      float4 la = nd[0], lb = nd[1], ra = nd[2], rb = nd[3];
+      int lref = __float_as_int(la.w), rref = __float_as_int(lb.w);
+      float t0l, t0r;
+      float d1 = hitAABB(o, inv, la, lb, t0l);
+      float d2 = hitAABB(o, inv, ra, rb, t0r);
+      bool h1 = (lref != REF_NONE) && d1 > 0.0f;
+      bool h2 = (rref != REF_NONE) && d2 > 0.0f;
+      if (COUNT) C.nodes += 1u + (lref != REF_NONE) + (rref != REF_NONE);
+      if (CULL) {
+        float lim = tbest + 1e-3f * fmaxf(1.0f, tbest);
+        h1 = h1 && !(t0l > lim);
+        h2 = h2 && !(t0r > lim);
+      }
+      if (h1 && h2) {
+        bool leftFirst = d1 < d2;
+        st.push(leftFirst ? rref : lref);
+        ref = leftFirst ? lref : rref;
+        continue;
+      }
+      if (h1) { ref = lref; continue; }
+      if (h2) { ref = rref; continue; }
+    } else if (ref != REF_NONE) {
+      uint32_t v = ~(uint32_t)ref;
+      int start = (int)(v >> LEAF_CNT_BITS);
+      int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
+      if (COUNT) C.nodes++;
+      float localBest = PT_INF;
+      for (int k = 0; k < cnt; k++) {
+        int i = start + k;
+        float t;
+        bool hit = triHit(S.geo + 4 * (size_t)i, o, d, t);
+        if (COUNT) {
+          C.tris++;
+          if (hit && t < localBest) { localBest = t; C.mats++; }
+        }
+        if (hit && t < tbest) {
+          tbest = t;
+          best = i;
+          if (ANYHIT) { tOut = tbest; return best; }
+        }
+      }
+    }
+    if (st.sp == 0) break;
+    ref = st.pop();
+  }
+  tOut = tbest;
+  return best;
+}
+
+// The full HitResult (IS:63-71) of the winning triangle, computed once.
+struct Hit {
+  V3 P, N, viewDir;
+  Material m;
+};
+__device__ __forceinline__ void finishHit(const SceneView& S, int tri, V3 o, V3 d, float t, Hit& h) {
+  const float4* g = S.geo + 4 * (size_t)tri;
+  float4 A = g[0], B = g[1], C4 = g[2], Nn = g[3];
+  V3 p1 = v3(A.x, A.y, A.z), p2 = v3(B.x, B.y, B.z), p3 = v3(C4.x, C4.y, C4.z);
+  bool inside = dot(v3(Nn.x, Nn.y, Nn.z), d) > 0.0f;
+  V3 P = o + d * t;
+  float alpha = (-(P.x - p2.x) * (p3.y - p2.y) + (P.y - p2.y) * (p3.x - p2.x)) /
+                (-(p1.x - p2.x - 0.00005f) * (p3.y - p2.y + 0.00005f) + (p1.y - p2.y + 0.00005f) * (p3.x - p2.x + 0.00005f));
+  float beta = (-(P.x - p3.x) * (p1.y - p3.y) + (P.y - p3.y) * (p1.x - p3.x)) /
+               (-(p2.x - p3.x - 0.00005f) * (p1.y - p3.y + 0.00005f) + (p2.y - p3.y + 0.00005f) * (p1.x - p3.x + 0.00005f));
+  float gama = 1.0f - alpha - beta;
+  const float* rec = S.attr + 36 * (size_t)tri;
+  const float4* q = reinterpret_cast<const float4*>(rec + 8);
+  float4 q0 = q[0], q1 = q[1], q2 = q[2];  // floats 8..19
+  V3 n1 = v3(q0.y, q0.z, q0.w), n2 = v3(q1.x, q1.y, q1.z), n3 = v3(q1.w, q2.x, q2.y);
+  V3 Ns = normalize((n1 * alpha + n2 * beta) + n3 * gama);
+  h.P = P;
+  h.N = inside ? -Ns : Ns;
+  h.viewDir = d;
+  h.m = loadMaterial(rec);
+}
+
+}  // namespace pt

@@ -104,6 +104,7 @@ def test_tile_shards_reassemble_bit_exact(world):
         n = r.owned_pixel_count()
         assert n == D.packed_count(w, h, k, world)
         t = torch.zeros((n, 4), dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()  # the fill runs on torch's stream, the pack on the renderer's
         r.pack_owned(t.data_ptr())
         r.synchronize()
         assert np.array_equal(t.cpu().numpy(), D.pack(ref, k, world))
