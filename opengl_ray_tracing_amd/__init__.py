@@ -6,11 +6,11 @@ C ABI of libpt.so. There is no CPU fallback in this package.
 """
 from .scene import (Material, Scene, calculate_hdr_cache, decode_hdr, get_transform_matrix, load_hdr,
                     orbit_camera)
-from .renderer import (FLAG_CLOSEST_SHADOW, FLAG_COUNT_FETCHES, FLAG_WAVEFRONT, FLAG_NO_CULL, INTEGRATORS, FrameStats, Renderer,
+from .renderer import (FLAG_CLOSEST_SHADOW, FLAG_COUNT_FETCHES, FLAG_REGEN, FLAG_WAVEFRONT, FLAG_NO_CULL, INTEGRATORS, FrameStats, Renderer,
                        device_count)
 
 __all__ = [
     "Material", "Scene", "calculate_hdr_cache", "decode_hdr", "get_transform_matrix", "load_hdr", "orbit_camera",
     "Renderer", "FrameStats", "device_count", "INTEGRATORS", "FLAG_NO_CULL", "FLAG_CLOSEST_SHADOW",
-    "FLAG_COUNT_FETCHES", "FLAG_WAVEFRONT",
+    "FLAG_COUNT_FETCHES", "FLAG_REGEN", "FLAG_WAVEFRONT",
 ]

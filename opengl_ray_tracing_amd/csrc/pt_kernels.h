@@ -55,6 +55,7 @@ struct RenderParams {
   int* ovf;             // traversal stack overflow (per thread ovfDepth ints), may be null
   int ovfDepth;
   unsigned long long* stats;  // [rays, nodes, tris, mats, texels]
+  unsigned long long* rayShards;  // 64 sharded ray counters (regen kernel)
 };
 
 struct TraceParams {
@@ -85,6 +86,9 @@ struct PackParams {
 
 hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count);
 hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, int* nb);
+hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull);
+hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb);
+int regenLdsStack();
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s);

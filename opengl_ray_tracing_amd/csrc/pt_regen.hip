@@ -1,0 +1,319 @@
+// pt_regen.hip -- frame kernel selected by PT_FLAG_REGEN: a persistent path state machine
+// with per-lane path regeneration.
+//
+// Every lane owns one path at a time and runs one loop: trace the lane's
+// current ray (closest hit, or any hit for an env shadow ray) through the single
+// traversal call site, then advance the path by one event (primary hit/miss,
+// bounce hit/miss, shadow result). A lane whose path has ended writes its
+// pixel's running mean and immediately takes the next pixel of its wave's 8x8
+// tile (ballot + prefix over the idle lanes); a wave takes a new tile from the
+// per-XCD-group work queues when its tile is used up. Lanes therefore never
+// idle while their neighbours finish longer paths, and only path state (not the
+// traversal or BRDF temporaries) is live across the traversal loop, which keeps
+// the register file -- and so occupancy -- well below the one-call-per-bounce
+// megakernel's.
+//
+// Per path the sequence of random numbers, rays and floating-point operations
+// is exactly that of main()/pathTracing*() in pass1.fsh (and of the lock-step
+// megakernel in pt_kernels.hip and the CPU checker), so images are bit-identical.
+// Reference: ImportanceSampling_LowDiscrepancySequence/shaders/pass1.fsh (IS)
+// main IS:844-872, pathTracingImportanceSampling IS:761-841; DisneyBRDF
+// pathTracing D:443-481; OpenglRayTracing pathTracing O:329-364.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_device.h"
+#include "pt_kernels.h"
+#include "pt_trace.h"
+
+namespace pt {
+
+#ifndef PT_REGEN_LDS_STACK
+#define PT_REGEN_LDS_STACK 16
+#endif
+constexpr int REGEN_LDS_STACK = PT_REGEN_LDS_STACK;
+// minimum waves per SIMD the register allocator must allow (uniform integrators
+// fit 128 VGPRs without spilling; the MIS state machine does not)
+#ifndef PT_REGEN_MIN_WAVES_U
+#define PT_REGEN_MIN_WAVES_U 4
+#endif
+#ifndef PT_REGEN_MIN_WAVES_MIS
+#define PT_REGEN_MIN_WAVES_MIS 1
+#endif
+
+enum : int { K_NONE = 0, K_PRIMARY = 1, K_BOUNCE = 2, K_SHADOW = 3 };
+
+struct PathState {
+  int px, py;
+  int kind;      // the ray in flight (K_*)
+  int bounce;    // bounce index of the K_BOUNCE / K_SHADOW ray
+  uint32_t seed;
+  V3 o, d;       // ray in flight
+  V3 Lo, hist, Le0;
+  V3 f_r;        // BRDF value of the bounce ray in flight
+  float cosL;    // cosine_i (uniform) / NdotL (MIS) of the bounce ray
+  float pdfB;    // pdf_brdf of the MIS bounce ray
+  V3 Lb;         // MIS: the BRDF ray traced after the shadow ray
+  V3 shC;        // MIS: unoccluded env contribution of the shadow ray
+  bool haveB;    // MIS: a BRDF ray follows the shadow ray
+};
+
+__device__ __forceinline__ void writeAccum(const RenderParams& p, int px, int py, V3 color) {
+  float4* a = p.accum + (size_t)py * p.width + px;
+  float4 old = *a;
+  float w = 1.0f / (float)(p.frameCounter + 1u);
+  *a = make_float4(mixf(old.x, color.x, w), mixf(old.y, color.y, w), mixf(old.z, color.z, w), 1.0f);
+}
+
+// main IS:846-850: seed and camera ray of pixel (px, py)
+__device__ __forceinline__ void startPath(const RenderParams& p, PathState& s) {
+  const int W = p.width, H = p.height;
+  s.seed = ((uint32_t)s.px * 1973u + (uint32_t)s.py * 9277u + p.frameCounter * 26699u) | 1u;
+  float pixx = (float)(2 * s.px + 1) / (float)W - 1.0f;
+  float pixy = (float)(2 * s.py + 1) / (float)H - 1.0f;
+  float ax = (randf(s.seed) - 0.5f) / (float)W;
+  float ay = (randf(s.seed) - 0.5f) / (float)H;
+  float x = pixx + ax, y = pixy + ay, z = -1.5f;
+  const float* M = p.cam;
+  V3 c0 = v3(M[0], M[1], M[2]), c1 = v3(M[4], M[5], M[6]), c2 = v3(M[8], M[9], M[10]), c3 = v3(M[12], M[13], M[14]);
+  s.d = normalize((c0 * x + c1 * y) + (c2 * z + c3 * 0.0f));
+  s.o = v3(p.eye[0], p.eye[1], p.eye[2]);
+  s.kind = K_PRIMARY;
+  s.bounce = 0;
+  s.Lo = v3(0, 0, 0);
+  s.hist = v3(1, 1, 1);
+}
+
+// The path has a new surface hit `hit` at bounce index nb: sample the next
+// ray(s) (O:335-345, D:448-456, IS:766-816) or end the path. Returns false when
+// the path ends.
+template <int INTEG>
+__device__ __forceinline__ bool continueFromHit(const RenderParams& p, PathState& s, const Hit& hit, int nb) {
+  if (nb >= p.maxBounce) return false;
+  s.bounce = nb;
+  s.o = hit.P;
+  if (INTEG != 2) {
+    V3 N = hit.N;
+    V3 L = toNormalHemisphere(sampleHemisphereRand(s.seed), N);
+    s.cosL = fmaxf(0.0f, dot(L, N));
+    if (INTEG == 0) {
+      s.f_r = hit.m.baseColor / PT_PI;
+    } else {
+      V3 tangent, bitangent;
+      getTangent(N, tangent, bitangent);
+      s.f_r = brdfAniso(-hit.viewDir, N, L, tangent, bitangent, hit.m);
+    }
+    s.d = L;
+    s.kind = K_BOUNCE;
+    return true;
+  }
+  V3 V = -hit.viewDir;
+  V3 N = hit.N;
+  float r1 = randf(s.seed);
+  float r2 = randf(s.seed);
+  V3 Ldir = sampleHdrDir(p.env, r1, r2);
+  bool shadow = false;
+  if (dot(N, Ldir) > 0.0f) {  // IS:775-790; added if the shadow ray escapes
+    V3 L = Ldir;
+    V3 color = hdrColor(p.env, L);
+    float pdf_light = hdrPdf(p.env, L);
+    V3 f_r = brdfIso(V, N, L, hit.m);
+    float pdf_brdf = brdfPdf(V, N, L, hit.m);
+    float mis_weight = misWeight(pdf_light, pdf_brdf);
+    V3 c = ((s.hist * mis_weight) * color) * f_r;
+    s.shC = (c * dot(N, L)) / pdf_light;
+    shadow = true;
+  }
+  const uint32_t gi = grayCode(p.frameCounter + 1u);
+  float u = sobolf(2u * (uint32_t)nb, gi);
+  float v = sobolf(2u * (uint32_t)nb + 1u, gi);
+  cranleyPatterson(s.px, s.py, u, v);
+  float xi_3 = randf(s.seed);
+  V3 L = sampleBRDF(u, v, xi_3, V, N, hit.m);
+  float NdotL = dot(N, L);
+  s.haveB = false;
+  if (NdotL > 0.0f) {
+    V3 f_r = brdfIso(V, N, L, hit.m);
+    float pdf_brdf = brdfPdf(V, N, L, hit.m);
+    // IS:816: pdf <= 0 ends the path (the reference traces the ray first and discards it)
+    if (pdf_brdf > 0.0f) {
+      s.f_r = f_r;
+      s.cosL = NdotL;
+      s.pdfB = pdf_brdf;
+      s.Lb = L;
+      s.haveB = true;
+    }
+  }
+  if (shadow) {
+    s.d = Ldir;
+    s.kind = K_SHADOW;
+    return true;
+  }
+  if (s.haveB) {
+    s.d = s.Lb;
+    s.kind = K_BOUNCE;
+    return true;
+  }
+  return false;
+}
+
+// Advance the path by the result (tri, t) of its ray in flight. Returns false
+// when the path has ended (its final color in `color`).
+template <int INTEG>
+__device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int tri, float t, V3& color) {
+  const SceneView& S = p.scene;
+  if (s.kind == K_SHADOW) {  // IS:776-790
+    if (tri < 0) s.Lo = s.Lo + s.shC;
+    if (!s.haveB) {
+      color = s.Le0 + s.Lo;
+      return false;
+    }
+    s.d = s.Lb;
+    s.kind = K_BOUNCE;
+    return true;
+  }
+  Hit hit;
+  if (s.kind == K_PRIMARY) {
+    if (tri < 0) {  // IS:857-859
+      color = sampleHdr(p.env, s.d);
+      return false;
+    }
+    finishHit(S, tri, s.o, s.d, t, hit);
+    s.Le0 = hit.m.emissive;
+    if (continueFromHit<INTEG>(p, s, hit, 0)) return true;
+    color = s.Le0 + s.Lo;
+    return false;
+  }
+  // K_BOUNCE
+  if (INTEG == 2) {
+    if (tri < 0) {  // IS:819-829
+      V3 c = hdrColor(p.env, s.d);
+      float pdf_light = hdrPdf(p.env, s.d);
+      float mis_weight = misWeight(s.pdfB, pdf_light);
+      V3 cc = ((s.hist * mis_weight) * c) * s.f_r;
+      s.Lo = s.Lo + (cc * s.cosL) / s.pdfB;
+      color = s.Le0 + s.Lo;
+      return false;
+    }
+    finishHit(S, tri, s.o, s.d, t, hit);  // IS:833-837
+    V3 Le = hit.m.emissive;
+    s.Lo = s.Lo + ((s.hist * Le) * s.f_r * s.cosL) / s.pdfB;
+    s.hist = s.hist * ((s.f_r * s.cosL) / s.pdfB);
+  } else {  // O:347-360 / D:463-479
+    const float pdf = 1.0f / (2.0f * PT_PI);
+    if (tri < 0) {
+      V3 sky = sampleHdr(p.env, s.d);
+      s.Lo = s.Lo + ((s.hist * sky) * s.f_r * s.cosL) / pdf;
+      color = s.Le0 + s.Lo;
+      return false;
+    }
+    finishHit(S, tri, s.o, s.d, t, hit);
+    V3 Le = hit.m.emissive;
+    s.Lo = s.Lo + ((s.hist * Le) * s.f_r * s.cosL) / pdf;
+    s.hist = s.hist * ((s.f_r * s.cosL) / pdf);
+  }
+  if (continueFromHit<INTEG>(p, s, hit, s.bounce + 1)) return true;
+  color = s.Le0 + s.Lo;
+  return false;
+}
+
+template <int INTEG, bool CULL>
+__global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U) void regenKernel(RenderParams p) {
+  __shared__ int s_stack[REGEN_LDS_STACK * BLOCK];
+  StackT<REGEN_LDS_STACK, BLOCK> st;
+  st.lds = s_stack + threadIdx.x;
+  st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * p.ovfDepth : nullptr;
+  st.sp = 0;
+  Counters C = {0, 0, 0, 0, 0};
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const int home = blockIdx.x & (NUM_QUEUES - 1);
+  const int sub = p.shardSize >> 3;
+  int qi = 0;         // queues tried (wave-uniform)
+  int tile = -1;      // current 8x8 wave tile (wave-uniform)
+  int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
+  bool active = false;
+  PathState s;
+  s.px = s.py = 0;
+  s.kind = K_NONE;
+  while (true) {
+    // regenerate: idle lanes take the next pixels of the wave's tile
+    while (true) {
+      const unsigned long long idle = __ballot(!active);
+      if (idle == 0) break;
+      if (cursor >= 64) {
+        int item = -1;
+        while (qi < NUM_QUEUES) {
+          const int q = (home + qi) & (NUM_QUEUES - 1);
+          int it = 0;
+          if (lane == 0) it = atomicAdd(p.queue + q, 1);
+          it = __shfl(it, 0, 64);
+          if (it < p.perQueue && q * p.perQueue + it < p.numItems) {
+            item = q * p.perQueue + it;
+            break;
+          }
+          qi++;
+        }
+        if (item < 0) break;  // no tiles left for this wave
+        tile = item;
+        cursor = 0;
+      }
+      const int slot = cursor + __popcll(idle & below);
+      if (!active && slot < 64) {
+        const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
+        const int g = j * p.world + p.rank;
+        const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
+        const int px = gx * p.shardSize + (sI % sub) * 8 + (slot & 7);
+        const int py = gy * p.shardSize + (sI / sub) * 8 + (slot >> 3);
+        if (px < p.width && py < p.height) {
+          s.px = px;
+          s.py = py;
+          startPath(p, s);
+          active = true;
+        }
+      }
+      cursor = min(64, cursor + __popcll(idle));
+    }
+    if (__ballot(active) == 0) break;
+    if (!active) continue;
+    float t;
+    const int tri = traceRay<false, CULL, false>(p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW);
+    V3 color;
+    if (!advance<INTEG>(p, s, tri, t, color)) {
+      writeAccum(p, s.px, s.py, color);
+      active = false;
+    }
+  }
+  uint32_t r = C.rays;
+  for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
+  if (lane == 0 && r) atomicAdd(p.rayShards + (blockIdx.x & 63), (unsigned long long)r);
+}
+
+template <int I>
+static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull) {
+  if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
+  else hipLaunchKernelGGL((regenKernel<I, false>), dim3(grid), dim3(BLOCK), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull) {
+  switch (integrator) {
+    case 0: return launchRegenI<0>(p, grid, s, cull);
+    case 1: return launchRegenI<1>(p, grid, s, cull);
+    default: return launchRegenI<2>(p, grid, s, cull);
+  }
+}
+
+hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb) {
+  const void* f;
+  switch (integrator) {
+    case 0: f = cull ? (const void*)regenKernel<0, true> : (const void*)regenKernel<0, false>; break;
+    case 1: f = cull ? (const void*)regenKernel<1, true> : (const void*)regenKernel<1, false>; break;
+    default: f = cull ? (const void*)regenKernel<2, true> : (const void*)regenKernel<2, false>; break;
+  }
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, f, BLOCK, 0);
+}
+
+int regenLdsStack() { return REGEN_LDS_STACK; }
+
+}  // namespace pt

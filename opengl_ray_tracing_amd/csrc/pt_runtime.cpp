@@ -513,12 +513,16 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   const bool cull = !count && !(c.flags & PT_FLAG_NO_CULL);
   if (!count && (c.flags & PT_FLAG_WAVEFRONT))
     return renderWavefront(ctx, eye, cameraRotate, frameCounter, cull, stats, evb, eve);
+  // default: the lock-step persistent megakernel (also the fetch-counting
+  // variant); the path-regeneration kernel on request
+  const bool regen = !count && (c.flags & PT_FLAG_REGEN);
   int nb = 0;
-  CK(renderBlocksPerCU(c.integrator, cull, count, &nb));
+  if (regen) CK(regenBlocksPerCU(c.integrator, cull, &nb));
+  else CK(renderBlocksPerCU(c.integrator, cull, count, &nb));
   if (nb < 1) nb = 1;
   int grid = ctx->numCU * nb;
   int ovfDepth = 0;
-  int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth);
+  int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK);
   if (rc) return rc;
   RenderParams p;
   std::memset(&p, 0, sizeof(p));
@@ -546,8 +550,10 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   p.ovf = ovfDepth ? ctx->d_ovf : nullptr;
   p.ovfDepth = ovfDepth;
   p.stats = stats;
+  p.rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAY_SHARDS);
   CK(hipEventRecord(evb, ctx->stream));
-  CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
+  if (regen) CK(launchRegen(p, c.integrator, grid, ctx->stream, cull));
+  else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
   CK(hipEventRecord(eve, ctx->stream));
   ctx->launches++;
   return PT_OK;

@@ -80,9 +80,11 @@ __device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float& t) {
 // first, ties to the right child), strict '<' closest update, so the same
 // triangle wins. CULL skips children whose slab entry lies beyond the current
 // closest hit (plus a margin); ANYHIT returns on the first accepted triangle
-// (used for env shadow rays, where only isHit is read: IS:776-779).
+// (used for env shadow rays, where only isHit is read: IS:776-779); anyRT is
+// the same switch chosen per lane at run time (one call site for both kinds).
 template <bool ANYHIT, bool CULL, bool COUNT, class StackType>
-__device__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C) {
+__device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
+                                        bool anyRT = false) {
   V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float tbest = PT_INF;
   int best = -1;
@@ -130,7 +132,7 @@ __device__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& 
         if (hit && t < tbest) {
           tbest = t;
           best = i;
-          if (ANYHIT) { tOut = tbest; return best; }
+          if (ANYHIT || anyRT) { tOut = tbest; return best; }
         }
       }
     }

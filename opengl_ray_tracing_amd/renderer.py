@@ -29,6 +29,7 @@ FLAG_NO_CULL = 0x1
 FLAG_CLOSEST_SHADOW = 0x2
 FLAG_COUNT_FETCHES = 0x4
 FLAG_WAVEFRONT = 0x8
+FLAG_REGEN = 0x10
 
 
 @dataclass

@@ -110,16 +110,20 @@ def test_fetch_counts_match_oracle(c2):
 
 
 @pytest.mark.parametrize("name,integrator", [("c2", "lambert"), ("c3", "disney"), ("c3", "mis"), ("c4", "mis")])
-def test_wavefront_equals_megakernel(request, name, integrator):
-    """The wavefront pipeline (FLAG_WAVEFRONT) and the persistent megakernel (default) give identical images."""
-    from opengl_ray_tracing_amd import FLAG_WAVEFRONT
+def test_frame_kernels_agree(request, name, integrator):
+    """The lock-step megakernel (default), the path-regeneration kernel (FLAG_REGEN) and the
+    wavefront pipeline (FLAG_WAVEFRONT) give bit-identical images."""
+    from opengl_ray_tracing_amd import FLAG_REGEN, FLAG_WAVEFRONT
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     mb = {"disney": 5}.get(integrator, cfg.max_bounce)
-    a, sa = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_WAVEFRONT)
+    a, sa = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_REGEN)
     b, sb = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb)
+    c, sc = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_WAVEFRONT)
     assert np.array_equal(a, b)
+    assert np.array_equal(c, b)
     if integrator == "mis":
-        # the wavefront path skips BRDF rays whose pdf is 0 (IS:816 discards them after tracing)
-        assert sa.rays <= sb.rays and sa.rays >= 0.95 * sb.rays
+        # regeneration and wavefront skip BRDF rays whose pdf is 0 (IS:816 discards them after tracing)
+        assert sa.rays == sc.rays
+        assert sb.rays >= sa.rays >= 0.95 * sb.rays
     else:
-        assert sa.rays == sb.rays
+        assert sa.rays == sb.rays == sc.rays
