@@ -41,8 +41,10 @@ def parse():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--builder", default=None, help="override the config's BVH builder")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=2, help="cpu_baseline sample: full frames rendered")
-    ap.add_argument("--traffic", default=None, help="JSON file with per-launch PMC HBM bytes (profiles/)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="cpu_baseline sample: full frames are rendered until this much CPU wall time has passed")
+    ap.add_argument("--traffic", default=str(ROOT / "profiles" / "r1" / "traffic.json"),
+                    help="JSON with per-launch PMC HBM bytes of the bench kernel (tools/traffic.py)")
     ap.add_argument("--flags", type=int, default=0)
     return ap.parse_args()
 
@@ -89,24 +91,17 @@ def main():
     rc.close()
     bytes_per_ray = (48 * cs.node_fetch + 72 * cs.tri_fetch + 72 * cs.mat_fetch + 12 * cs.tex_fetch) / max(cs.rays, 1)
 
-    # ---- multi-GPU gather buffers (screen-tile shards)
+    # ---- multi-GPU: RCCL gather of every rank's screen-tile shard to rank 0;
+    # the renderer runs on torch's current stream so the collective orders after the frame
+    gather = None
     if n > 1:
-        counts = [r.owned_pixel_count(k, n) for k in range(n)]
-        maxc = max(counts)
-        send = torch.zeros((maxc, 4), dtype=torch.float32, device=f"cuda:{local}")
-        gather = [torch.zeros((maxc, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n)] \
-            if rank == 0 else None
-        stream = torch.cuda.current_stream().cuda_stream
-        r.set_stream(stream)
+        from opengl_ray_tracing_amd.distributed import FrameGather
+        gather = FrameGather(r, rank, n, f"cuda:{local}")
 
     def step(frame):
         r.render_frame(eye, rot, frame, sync=False)
-        if n > 1:
-            r.pack_owned(send.data_ptr())
-            dist.gather(send, gather_list=gather, dst=0)
-            if rank == 0:
-                for k in range(1, n):
-                    r.unpack_rank(k, n, gather[k].data_ptr())
+        if gather is not None:
+            gather()
 
     def sync_all():
         r.synchronize()
@@ -147,15 +142,16 @@ def main():
         rays_per_launch = rays_local / max(st.launches, 1)
         achieved = rays_per_launch * bytes_per_ray / (kernel_ms_avg * 1e-3) / 1e9
         traffic = None
-        if args.traffic and Path(args.traffic).exists():
-            traffic = json.loads(Path(args.traffic).read_text()).get(args.config)
+        if args.traffic and Path(args.traffic).exists() and not args.flags and not args.builder:
+            ent = json.loads(Path(args.traffic).read_text()).get(args.config)
+            traffic = ent.get("bytes_per_launch") if ent else None
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": "renderKernel<%s>" % cfg.integrator, "kernel_ms": round(kernel_ms_avg, 4),
                     "bytes_per_ray": round(bytes_per_ray, 1), "rays_per_launch": int(rays_per_launch)}
         cpu = None
         if not args.no_cpu_baseline and n == 1:
-            cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_frames)
+            cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_seconds)
         line = {
             "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
@@ -173,9 +169,10 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, frames):
+def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, seconds):
     """The CPU restatement of the reference (oracle/, test infrastructure) timed on the host
-    cores: `frames` full frames of the same workload, OpenMP over pixels."""
+    cores: full frames of the same workload (same scene, camera, frame sequence), OpenMP over
+    pixels, until `seconds` of wall time have passed (a bounded sample)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle  # noqa: E402  (bench.py's cpu_baseline leg is the only bench use of oracle/)
 
@@ -187,11 +184,15 @@ def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, frames):
     orc = oracle.Oracle(tris, nodes, hdr)
     acc = np.zeros((cfg.height, cfg.width, 4), np.float32)
     rays = 0
+    frames = 0
     t0 = time.perf_counter()
-    for f in range(frames):
-        acc, c = orc.render(cfg.width, cfg.height, cfg.integrator, f, eye, rot, accum=acc,
+    while True:
+        acc, c = orc.render(cfg.width, cfg.height, cfg.integrator, frames, eye, rot, accum=acc,
                             max_bounce=cfg.max_bounce, threads=cores)
         rays += c.rays
+        frames += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
     dt = time.perf_counter() - t0
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"{frames} full {cfg.width}x{cfg.height} frames of {cfg.name} ({rays} rays, {dt:.1f} s)",

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the bench kernel from the rocprofv3 FETCH_SIZE /
+WRITE_SIZE passes of tools/gpu_profile.sh, corrected as MI355X_MICROARCH.md
+("HBM [CDNA4]") prescribes: both counters are in KiB; on gfx950 FETCH_SIZE
+reports half the bytes of wide reads, so it is doubled; WRITE_SIZE is exact.
+
+    python tools/traffic.py <prof_dir> <config> <out.json>
+
+Merges {config: {...}} into out.json (read by bench.py --traffic).
+"""
+import csv
+import glob
+import json
+import sys
+from pathlib import Path
+
+
+def per_launch(d, counter, kernel_pat):
+    vals = []
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter and kernel_pat in r["Kernel_Name"]:
+                vals.append((r["Kernel_Name"], float(r["Counter_Value"])))
+    return vals
+
+
+def main():
+    d, cfg, out = sys.argv[1], sys.argv[2], Path(sys.argv[3])
+    pat = "renderKernel<"
+    fe = [v for k, v in per_launch(f"{d}/fetch", "FETCH_SIZE", pat) if k.endswith("true, false>(pt::RenderParams)")]
+    wr = [v for k, v in per_launch(f"{d}/write", "WRITE_SIZE", pat) if k.endswith("true, false>(pt::RenderParams)")]
+    if not fe or not wr:
+        raise SystemExit("no bench-kernel dispatches found")
+    f_kb, w_kb = sum(fe) / len(fe), sum(wr) / len(wr)
+    ent = {"kernel": "renderKernel<*, CULL, !COUNT>", "launches": [len(fe), len(wr)],
+           "fetch_size_kb": round(f_kb, 1), "write_size_kb": round(w_kb, 1),
+           "bytes_per_launch": int((2 * f_kb + w_kb) * 1024),
+           "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, KiB units)"}
+    data = json.loads(out.read_text()) if out.exists() else {}
+    data[cfg] = ent
+    out.write_text(json.dumps(data, indent=1) + "\n")
+    print(cfg, ent)
+
+
+if __name__ == "__main__":
+    main()
