@@ -57,14 +57,16 @@ __device__ __forceinline__ float hitAABB(V3 o, V3 inv, float4 lo, float4 hi, flo
 // normal Ng = normalize(cross(p2-p1,p3-p1)) and w = dot(Ng,p1) (computed on the
 // host in the reference's order) this rounds exactly like the reference: the
 // orientation flip negates numerator, denominator and all three edge tests
-// exactly, so it changes neither t nor the accept decision.
-__device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float& t) {
+// exactly, so it changes neither t nor the accept decision. A triangle at or
+// beyond tmax cannot win (the caller keeps a hit only if t < tbest), so it is
+// rejected before the edge tests; pass PT_INF to get the plain hitTriangle.
+__device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, float& t) {
   float4 A = g[0], B = g[1], C = g[2], Nn = g[3];
   V3 N = v3(Nn.x, Nn.y, Nn.z);
   float dn = dot(N, d);
   if (fabsf(dn) < 0.00001f) return false;
   float tt = (A.w - dot(o, N)) / dn;
-  if (tt < 0.0005f) return false;
+  if (tt < 0.0005f || !(tt < tmax)) return false;
   V3 p1 = v3(A.x, A.y, A.z), p2 = v3(B.x, B.y, B.z), p3 = v3(C.x, C.y, C.z);
   V3 P = o + d * tt;
   float s1 = dot(cross(p2 - p1, P - p1), N);
@@ -76,23 +78,36 @@ __device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float& t) {
   return r1 || r2;
 }
 
-// hitBVH IS:335-382: same visiting order (nearer child by the reference's d
-// first, ties to the right child), strict '<' closest update, so the same
-// triangle wins. CULL skips children whose slab entry lies beyond the current
-// closest hit (plus a margin); ANYHIT returns on the first accepted triangle
-// (used for env shadow rays, where only isHit is read: IS:776-779); anyRT is
-// the same switch chosen per lane at run time (one call site for both kinds).
+__device__ __forceinline__ bool isLeafRef(int ref) { return ref < 0 && ref != REF_NONE; }
+
+// hitBVH IS:335-382: same visiting order of the leaves (nearer child by the
+// reference's d first, ties to the right child), strict '<' closest update, so
+// the same triangle wins even on exact-t ties. CULL skips children whose slab
+// entry lies beyond the current closest hit (plus a margin, so tied triangles
+// are still visited); ANYHIT returns on the first accepted triangle (env shadow
+// rays, where only isHit is read: IS:776-779); anyRT is the same switch chosen
+// per lane at run time.
+//
+// Loop structure ("while-while" with speculative node traversal): a lane that
+// reaches a leaf parks it and keeps visiting the nodes that follow it in the
+// visiting order until every lane still walking nodes holds a parked leaf; the
+// wave then intersects the parked leaves together. Leaves are still intersected
+// in the reference's order (the parked leaf precedes every node visited
+// speculatively); node visits use a possibly stale tbest for culling, which
+// only culls less.
 template <bool ANYHIT, bool CULL, bool COUNT, class StackType>
 __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
                                         bool anyRT = false) {
   V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float tbest = PT_INF;
   int best = -1;
-  int ref = S.rootRef;
+  int ref = S.rootRef;   // next item in visiting order (REF_NONE only when the stack is empty too)
+  int leaf = REF_NONE;   // parked leaf, precedes ref
   st.sp = 0;
   C.rays++;
   while (true) {
-    if (ref >= 0) {
+    // node phase
+    while (ref >= 0) {
       const float4* nd = S.bvh + 4 * (size_t)ref;
       float4 la = nd[0], lb = nd[1], ra = nd[2], rb = nd[3];
       int lref = __float_as_int(la.w), rref = __float_as_int(lb.w);
@@ -107,37 +122,53 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
         h1 = h1 && !(t0l > lim);
         h2 = h2 && !(t0r > lim);
       }
+      int next;
       if (h1 && h2) {
         bool leftFirst = d1 < d2;
         st.push(leftFirst ? rref : lref);
-        ref = leftFirst ? lref : rref;
-        continue;
+        next = leftFirst ? lref : rref;
+      } else if (h1) {
+        next = lref;
+      } else if (h2) {
+        next = rref;
+      } else {
+        next = st.sp > 0 ? st.pop() : REF_NONE;
       }
-      if (h1) { ref = lref; continue; }
-      if (h2) { ref = rref; continue; }
-    } else if (ref != REF_NONE) {
-      uint32_t v = ~(uint32_t)ref;
+      if (isLeafRef(next) && leaf == REF_NONE) {  // park it, walk on
+        leaf = next;
+        next = st.sp > 0 ? st.pop() : REF_NONE;
+      }
+      ref = next;
+      if (__ballot(leaf == REF_NONE) == 0) break;  // every lane still walking holds a leaf
+    }
+    // leaf phase
+    if (leaf == REF_NONE && isLeafRef(ref)) {
+      leaf = ref;
+      ref = st.sp > 0 ? st.pop() : REF_NONE;
+    }
+    if (leaf == REF_NONE) break;  // ref == REF_NONE too: done
+    {
+      uint32_t v = ~(uint32_t)leaf;
       int start = (int)(v >> LEAF_CNT_BITS);
       int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
+      leaf = REF_NONE;
       if (COUNT) C.nodes++;
       float localBest = PT_INF;
       for (int k = 0; k < cnt; k++) {
         int i = start + k;
         float t;
-        bool hit = triHit(S.geo + 4 * (size_t)i, o, d, t);
         if (COUNT) {
+          bool hit = triHit(S.geo + 4 * (size_t)i, o, d, PT_INF, t);
           C.tris++;
           if (hit && t < localBest) { localBest = t; C.mats++; }
-        }
-        if (hit && t < tbest) {
+          if (hit && t < tbest) { tbest = t; best = i; }
+        } else if (triHit(S.geo + 4 * (size_t)i, o, d, tbest, t)) {
           tbest = t;
           best = i;
           if (ANYHIT || anyRT) { tOut = tbest; return best; }
         }
       }
     }
-    if (st.sp == 0) break;
-    ref = st.pop();
   }
   tOut = tbest;
   return best;

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(BLOCK) void wfTraceKernel(WFTraceParams p) {
     bool finished = false;
     if (leafI < leafEnd) {
       float t;
-      if (triHit(S.geo + 4 * (size_t)leafI, o, d, t) && t < tbest) {
+      if (triHit(S.geo + 4 * (size_t)leafI, o, d, tbest, t)) {
         tbest = t;
         best = leafI;
         if (ANYHIT) finished = true;

@@ -21,14 +21,15 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 
-def child(variant: str, config: str, frames: int, warmup: int, builder, flags: int = 0):
+def child(variant: str, config: str, frames: int, warmup: int, builder, flags: int = 0, max_bounce=None):
     from opengl_ray_tracing_amd import _native
     if variant != "base":
         _native.use_variant(variant)
     from opengl_ray_tracing_amd import Renderer, orbit_camera, scenes
     cfg, tris, nodes, hdr = scenes.build_config(config, builder)
     eye, rot = orbit_camera(*cfg.camera)
-    with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, flags=flags) as r:
+    mb = cfg.max_bounce if max_bounce is None else max_bounce
+    with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=mb, flags=flags) as r:
         r.upload_scene(tris, nodes)
         r.upload_env(hdr)
         for f in range(warmup):
@@ -39,7 +40,8 @@ def child(variant: str, config: str, frames: int, warmup: int, builder, flags: i
             r.render_frame(eye, rot, warmup + f, sync=False)
         st = r.stats()
     ms = st.kernel_ms_total / st.launches
-    print(json.dumps({"variant": variant, "flags": flags, "config": config, "kernel_ms": round(ms, 4),
+    print(json.dumps({"variant": variant, "flags": flags, "config": config, "max_bounce": mb, "kernel_ms": round(ms, 4),
+                      "rays": st.rays // max(st.launches, 1),
                       "mrays_s": round(st.rays / (st.kernel_ms_total * 1e-3) / 1e6, 1)}), flush=True)
 
 
@@ -53,10 +55,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--child", default=None)
+    ap.add_argument("--max-bounce", type=int, default=None)
     ap.add_argument("--flags", type=int, nargs="*", default=[0], help="renderer flags to A/B (e.g. 0 8)")
     a = ap.parse_args()
     if a.child:
-        child(a.child, a.config, a.frames, a.warmup, a.builder, a.flags[0])
+        child(a.child, a.config, a.frames, a.warmup, a.builder, a.flags[0], a.max_bounce)
         return
     if a.build is not None:
         from opengl_ray_tracing_amd import _build
@@ -70,7 +73,8 @@ def main():
     for _ in range(a.rounds):
         for (v, fl) in keys:
             cmd = [sys.executable, __file__, "--child", v, "--config", a.config, "--frames", str(a.frames),
-                   "--warmup", str(a.warmup), "--flags", str(fl)] + (["--builder", a.builder] if a.builder else [])
+                   "--warmup", str(a.warmup), "--flags", str(fl)] + (["--builder", a.builder] if a.builder else []) \
+                + (["--max-bounce", str(a.max_bounce)] if a.max_bounce is not None else [])
             out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
             if out.returncode != 0:
                 print(json.dumps({"variant": v, "flags": fl, "error": out.stderr[-2000:]}), flush=True)
