@@ -61,12 +61,13 @@ __device__ __forceinline__ float hitAABB(V3 o, V3 inv, float4 lo, float4 hi, flo
 // beyond tmax cannot win (the caller keeps a hit only if t < tbest), so it is
 // rejected before the edge tests; pass PT_INF to get the plain hitTriangle.
 __device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, float& t) {
+  // All four records are fetched together and every test is evaluated without
+  // branching: an early return would let the compiler sink the vertex loads
+  // behind the normal test, turning one memory round trip into three.
   float4 A = g[0], B = g[1], C = g[2], Nn = g[3];
   V3 N = v3(Nn.x, Nn.y, Nn.z);
   float dn = dot(N, d);
-  if (fabsf(dn) < 0.00001f) return false;
   float tt = (A.w - dot(o, N)) / dn;
-  if (tt < 0.0005f || !(tt < tmax)) return false;
   V3 p1 = v3(A.x, A.y, A.z), p2 = v3(B.x, B.y, B.z), p3 = v3(C.x, C.y, C.z);
   V3 P = o + d * tt;
   float s1 = dot(cross(p2 - p1, P - p1), N);
@@ -75,7 +76,7 @@ __device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, 
   bool r1 = (s1 > 0 && s2 > 0 && s3 > 0);
   bool r2 = (s1 < 0 && s2 < 0 && s3 < 0);
   t = tt;
-  return r1 || r2;
+  return !(fabsf(dn) < 0.00001f) && !(tt < 0.0005f) && (tt < tmax) && (r1 || r2);
 }
 
 __device__ __forceinline__ bool isLeafRef(int ref) { return ref < 0 && ref != REF_NONE; }
