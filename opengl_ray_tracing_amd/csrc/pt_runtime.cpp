@@ -197,8 +197,8 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
   if (nTri < 1 || nNodes < 2) return fail(ctx, PT_E_BADSCENE, "need >= 1 triangle and >= 2 nodes (dummy 0, root 1)");
   if (nTri > MAX_TRIS) return fail(ctx, PT_E_BADSCENE, "too many triangles for the leaf encoding");
   CK(hipSetDevice(ctx->cfg.device_id));
-  // geometry records
-  std::vector<float4> geo((size_t)nTri * 4);
+  // geometry records (+1 zero record: the leaf loop prefetches one record ahead)
+  std::vector<float4> geo((size_t)(nTri + 1) * 4, make_float4(0, 0, 0, 0));
   for (int i = 0; i < nTri; i++) {
     const float* t = tris + (size_t)i * 36;
     float N[3];

@@ -60,11 +60,10 @@ __device__ __forceinline__ float hitAABB(V3 o, V3 inv, float4 lo, float4 hi, flo
 // exactly, so it changes neither t nor the accept decision. A triangle at or
 // beyond tmax cannot win (the caller keeps a hit only if t < tbest), so it is
 // rejected before the edge tests; pass PT_INF to get the plain hitTriangle.
-__device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, float& t) {
-  // All four records are fetched together and every test is evaluated without
-  // branching: an early return would let the compiler sink the vertex loads
-  // behind the normal test, turning one memory round trip into three.
-  float4 A = g[0], B = g[1], C = g[2], Nn = g[3];
+__device__ __forceinline__ bool triTest(float4 A, float4 B, float4 C, float4 Nn, V3 o, V3 d, float tmax, float& t) {
+  // Every test is evaluated without branching: an early return would let the
+  // compiler sink the vertex loads behind the normal test, turning one memory
+  // round trip into three.
   V3 N = v3(Nn.x, Nn.y, Nn.z);
   float dn = dot(N, d);
   float tt = (A.w - dot(o, N)) / dn;
@@ -77,6 +76,9 @@ __device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, 
   bool r2 = (s1 < 0 && s2 < 0 && s3 < 0);
   t = tt;
   return !(fabsf(dn) < 0.00001f) && !(tt < 0.0005f) && (tt < tmax) && (r1 || r2);
+}
+__device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, float& t) {
+  return triTest(g[0], g[1], g[2], g[3], o, d, tmax, t);
 }
 
 __device__ __forceinline__ bool isLeafRef(int ref) { return ref < 0 && ref != REF_NONE; }
@@ -155,18 +157,37 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
       leaf = REF_NONE;
       if (COUNT) C.nodes++;
       float localBest = PT_INF;
-      for (int k = 0; k < cnt; k++) {
-        int i = start + k;
-        float t;
+      // two triangles per iteration, their eight records fetched together (one
+      // memory round trip per pair; the geometry buffer carries one zero record
+      // past the last triangle); tested in index order with the running tbest
+      for (int k = 0; k < cnt; k += 2) {
+        const int i = start + k;
+        const float4* g = S.geo + 4 * (size_t)i;
+        const float4 A0 = g[0], B0 = g[1], C0 = g[2], N0 = g[3];
+        const float4 A1 = g[4], B1 = g[5], C1 = g[6], N1 = g[7];
+        const bool second = k + 1 < cnt;
+        float t0, t1;
         if (COUNT) {
-          bool hit = triHit(S.geo + 4 * (size_t)i, o, d, PT_INF, t);
-          C.tris++;
-          if (hit && t < localBest) { localBest = t; C.mats++; }
-          if (hit && t < tbest) { tbest = t; best = i; }
-        } else if (triHit(S.geo + 4 * (size_t)i, o, d, tbest, t)) {
-          tbest = t;
-          best = i;
-          if (ANYHIT || anyRT) { tOut = tbest; return best; }
+          bool h0 = triTest(A0, B0, C0, N0, o, d, PT_INF, t0);
+          bool h1 = triTest(A1, B1, C1, N1, o, d, PT_INF, t1) & second;
+          C.tris += 1u + (second ? 1u : 0u);
+          if (h0 && t0 < localBest) { localBest = t0; C.mats++; }
+          if (h0 && t0 < tbest) { tbest = t0; best = i; }
+          if (h1 && t1 < localBest) { localBest = t1; C.mats++; }
+          if (h1 && t1 < tbest) { tbest = t1; best = i + 1; }
+        } else {
+          const bool h0 = triTest(A0, B0, C0, N0, o, d, tbest, t0);
+          if (h0) {
+            tbest = t0;
+            best = i;
+            if (ANYHIT || anyRT) { tOut = tbest; return best; }
+          }
+          const bool h1 = triTest(A1, B1, C1, N1, o, d, tbest, t1) & second;
+          if (h1) {
+            tbest = t1;
+            best = i + 1;
+            if (ANYHIT || anyRT) { tOut = tbest; return best; }
+          }
         }
       }
     }
