@@ -317,7 +317,11 @@ inline void grow(Box& b, f3 p) {
   b.lo = F3(gmin(b.lo.x, p.x), gmin(b.lo.y, p.y), gmin(b.lo.z, p.z));
   b.hi = F3(gmax(b.hi.x, p.x), gmax(b.hi.y, p.y), gmax(b.hi.z, p.z));
 }
-inline void grow(Box& b, const Box& o) { grow(b, o.lo); grow(b, o.hi); }
+inline void grow(Box& b, const Box& o) {
+  if (o.hi.x < o.lo.x) return;  // empty bin
+  grow(b, o.lo);
+  grow(b, o.hi);
+}
 inline float area(const Box& b) {
   if (b.hi.x < b.lo.x) return 0.0f;
   f3 d = b.hi - b.lo;
