@@ -2,10 +2,18 @@
 """Benchmark: Mrays/s and ms/frame at 1 spp per frame (BASELINE.json metric).
 
 A step is one progressive frame (one display() of OpenglRayTracing/main.cpp:558-603)
-of the configured workload: 1 spp for every pixel of the frame, running-mean
-accumulate, and for N > 1 ranks the RCCL gather of every rank's screen-tile
-shard to rank 0 (bit-exact reassembly). Default workload: configs[1] = c2,
-the OpenglRayTracing bunny scene (5k tris) at 1920x1080, Lambert, 2 bounces.
+of the configured workload on every rank: 1 spp for every pixel of the frame,
+running-mean accumulate. Default workload: configs[1] = c2, the
+OpenglRayTracing bunny scene (5k tris) at 1920x1080, Lambert, 2 bounces.
+
+N > 1 ranks (one process per GPU):
+  --shard samples (default, weak scaling): every rank renders the whole frame
+      from its own interleaved sample stream (rank r: samples r, r+N, ...), no
+      collective per step; the ranks' running means are combined by one RCCL
+      reduce after the timed steps (validated, not timed).
+  --shard tiles (strong scaling): every rank renders its 32x32 screen tiles of
+      the one frame; each step ends with the RCCL gather of the packed shards
+      to rank 0 (bit-exact reassembly).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver launch for N > 1)
@@ -46,6 +54,10 @@ def parse():
     ap.add_argument("--traffic", default=str(ROOT / "profiles" / "r1" / "traffic.json"),
                     help="JSON with per-launch PMC HBM bytes of the bench kernel (tools/traffic.py)")
     ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 on one GPU")
+    ap.add_argument("--same-device", action="store_true", help="rehearsal: every rank on device 0")
+    ap.add_argument("--shard", choices=["samples", "tiles"], default="samples",
+                    help="N > 1: sample-parallel full frames (weak) or screen-tile shards of one frame (strong)")
     return ap.parse_args()
 
 
@@ -72,18 +84,22 @@ def main():
     if n > 1:
         import torch
         import torch.distributed as dist
+        if args.same_device:
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(args.dist_backend, init_method="env://")
 
+    tiles = n > 1 and args.shard == "tiles"
+    split = dict(tile_rank=rank, tile_world=n) if tiles else dict(sample_rank=rank, sample_world=n)
     r = Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=local,
-                 tile_rank=rank, tile_world=n, flags=args.flags)
+                 flags=args.flags, **split)
     r.upload_scene(tris, nodes)
     r.upload_env(hdr)
 
     # ---- algorithmic bytes per ray of the reference algorithm, counted on the GPU by the
     # instrumented kernel variant (no culling, closest-hit shadows: exactly pass1.fsh's fetches)
     rc = Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=local,
-                  tile_rank=rank, tile_world=n, flags=FLAG_COUNT_FETCHES)
+                  flags=FLAG_COUNT_FETCHES, **split)
     rc.upload_scene(tris, nodes)
     rc.upload_env(hdr)
     rc.render_frame(eye, rot, 0)
@@ -93,10 +109,13 @@ def main():
 
     # ---- multi-GPU: RCCL gather of every rank's screen-tile shard to rank 0;
     # the renderer runs on torch's current stream so the collective orders after the frame
-    gather = None
-    if n > 1:
+    gather = combine = None
+    if tiles:
         from opengl_ray_tracing_amd.distributed import FrameGather
         gather = FrameGather(r, rank, n, f"cuda:{local}")
+    elif n > 1:
+        from opengl_ray_tracing_amd.distributed import SampleReduce
+        combine = SampleReduce(r, rank, n, f"cuda:{local}")
 
     def step(frame):
         r.render_frame(eye, rot, frame, sync=False)
@@ -120,11 +139,17 @@ def main():
     sync_all()
     t1 = time.perf_counter()
     st = r.stats()
+    combined_finite = None
+    if combine is not None:  # the ranks' running means -> one image on rank 0 (after the timed steps)
+        img = combine()
+        torch.cuda.synchronize()
+        combined_finite = bool(torch.isfinite(img).all().item()) if rank == 0 else None
 
     elapsed = t1 - t0
     rays_local = st.rays
     if n > 1:
-        tt = torch.tensor([elapsed, float(rays_local), st.kernel_ms_total], dtype=torch.float64, device=f"cuda:{local}")
+        dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{local}"
+        tt = torch.tensor([elapsed, float(rays_local), st.kernel_ms_total], dtype=torch.float64, device=dev)
         mx = tt.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tt.clone()
@@ -155,14 +180,20 @@ def main():
         line = {
             "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "strong" if args.shard == "tiles" else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
             "config": {"workload": f"{cfg.name}: {cfg.description}", "resolution": f"{cfg.width}x{cfg.height}",
                        "spp_per_frame": 1, "integrator": cfg.integrator, "max_bounce": cfg.max_bounce,
                        "triangles": int(tris.shape[0]), "bvh_nodes": int(nodes.shape[0]),
                        "bvh_builder": args.builder or cfg.builder, "env": cfg.env,
-                       "parallelism": f"screen-tile x{n}" + (" + RCCL gather" if n > 1 else "")},
+                       "parallelism": (f"screen-tile x{n}" + (" + RCCL gather per frame" if n > 1 else ""))
+                       if args.shard == "tiles" else
+                       (f"sample-parallel x{n}" + (" (RCCL reduce of the running means after the run)"
+                                                   if n > 1 else ""))},
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if combined_finite is not None:
+            line["config"]["combined_image_finite"] = combined_finite
         print(json.dumps(line), flush=True)
     r.close()
     if n > 1:

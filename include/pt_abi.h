@@ -63,6 +63,9 @@ typedef struct pt_config {
   uint32_t flags;     /* PT_FLAG_* */
   int basic_samples;  /* PT_BASIC_CPU_COMPAT: SAMPLE (BasicRayTracingWithC++/main.cpp:17), 0 = 128 */
   uint32_t basic_seed;/* PT_BASIC_CPU_COMPAT: seed of the per-pixel counter RNG */
+  int sample_rank;    /* sample-parallel rendering: this context draws the RNG/Sobol streams of   */
+  int sample_world;   /* samples frameCounter*sample_world + sample_rank (0/1 = the reference's   */
+                      /* frameCounter itself); the running-mean weight stays 1/(frameCounter+1)   */
 } pt_config;
 
 /* Counters accumulate over every launch since pt_create / pt_reset_stats. */
@@ -120,7 +123,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
 int pt_trace_closest(pt_ctx* ctx, const float* rays, int n, float* t_out, int* tri_out);
 
 /* Accumulation buffer access (lastFrame texture, main.cpp:763-764). */
-int pt_download_accum(pt_ctx* ctx, float* accum_rgba);
+int pt_download_accum(pt_ctx* ctx, float* accum_rgba);   /* host or device memory, width*height*4 f32 */
 int pt_upload_accum(pt_ctx* ctx, const float* accum_rgba);
 int pt_clear_accum(pt_ctx* ctx);
 int pt_accum_device_ptr(pt_ctx* ctx, void** dptr); /* width*height*4 f32, device memory */

@@ -22,6 +22,7 @@ class PtConfig(C.Structure):
         ("width", C.c_int), ("height", C.c_int), ("integrator", C.c_int), ("max_bounce", C.c_int),
         ("device_id", C.c_int), ("tile_rank", C.c_int), ("tile_world", C.c_int), ("tile_size", C.c_int),
         ("flags", C.c_uint32), ("basic_samples", C.c_int), ("basic_seed", C.c_uint32),
+        ("sample_rank", C.c_int), ("sample_world", C.c_int),
     ]
 
 
@@ -111,6 +112,20 @@ def lib_path() -> Path:
     return _build.variant_lib(_variant) if _variant else _build.LIB
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process. PyTorch-ROCm bundles its own libamdhip64
+    (its libraries ask for "libamdhip64.so", which does not match the
+    "libamdhip64.so.7" soname libpt.so asks for), so loading libpt.so before
+    torch puts two HIP/HSA runtimes in the process and whichever initialises
+    second can fail to see the GPU. Importing torch first makes libpt.so bind to
+    the already-loaded runtime (same soname). Without torch, libpt.so uses
+    /opt/rocm's runtime."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(build_if_missing: bool = False):
     """Load libpt.so (raises if absent: there is no CPU fallback)."""
     global _lib
@@ -121,6 +136,7 @@ def load(build_if_missing: bool = False):
         if not build_if_missing:
             raise RuntimeError(f"native library {path} is missing; run opengl_ray_tracing_amd._build.build_native()")
         _build.build_native()
+    _share_torch_hip_runtime()
     lib = C.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -40,7 +40,8 @@ struct RenderParams {
   SceneView scene;
   Env env;
   int width, height;
-  uint32_t frameCounter;
+  uint32_t frameCounter;  // running-mean count: weight 1/(frameCounter+1) (IS:868-871)
+  uint32_t sampleIndex;   // RNG / Sobol sample index: frameCounter*sample_world + sample_rank
   int maxBounce;
   float eye[3];
   float cam[16];

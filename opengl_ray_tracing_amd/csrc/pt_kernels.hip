@@ -108,7 +108,7 @@ template <class T>
 __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& seed, int px, int py,
                       uint32_t frameCounter, Counters& C, bool count) {
   V3 Lo = v3(0, 0, 0), history = v3(1, 1, 1);
-  const uint32_t gi = grayCode(frameCounter + 1u);
+  const uint32_t gi = grayCode(frameCounter + 1u);  // frameCounter = the sample index here
   for (int bounce = 0; bounce < maxBounce; bounce++) {
     V3 V = -hit.viewDir;
     V3 N = hit.N;
@@ -163,7 +163,7 @@ template <int INTEG, bool CULL, bool COUNT>
 __device__ __forceinline__ void shadePixel(const RenderParams& p, int px, int py, Stack& st, Counters& C) {
   Tracer<CULL, COUNT> tr{p.scene, st, C};
   const int W = p.width, H = p.height;
-  uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.frameCounter * 26699u) | 1u;
+  uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.sampleIndex * 26699u) | 1u;
   float pixx = (float)(2 * px + 1) / (float)W - 1.0f;
   float pixy = (float)(2 * py + 1) / (float)H - 1.0f;
   float ax = (randf(seed) - 0.5f) / (float)W;
@@ -183,7 +183,7 @@ __device__ __forceinline__ void shadePixel(const RenderParams& p, int px, int py
     V3 Li;
     if (INTEG == 0) Li = pathLambert(tr, p.env, first, p.maxBounce, seed, C, COUNT);
     else if (INTEG == 1) Li = pathDisneyUniform(tr, p.env, first, p.maxBounce, seed, C, COUNT);
-    else Li = pathMIS(tr, p.env, first, p.maxBounce, seed, px, py, p.frameCounter, C, COUNT);
+    else Li = pathMIS(tr, p.env, first, p.maxBounce, seed, px, py, p.sampleIndex, C, COUNT);
     color = first.m.emissive + Li;
   }
   float4* a = p.accum + (size_t)py * W + px;

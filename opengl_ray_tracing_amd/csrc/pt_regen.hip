@@ -68,7 +68,7 @@ __device__ __forceinline__ void writeAccum(const RenderParams& p, int px, int py
 // main IS:846-850: seed and camera ray of pixel (px, py)
 __device__ __forceinline__ void startPath(const RenderParams& p, PathState& s) {
   const int W = p.width, H = p.height;
-  s.seed = ((uint32_t)s.px * 1973u + (uint32_t)s.py * 9277u + p.frameCounter * 26699u) | 1u;
+  s.seed = ((uint32_t)s.px * 1973u + (uint32_t)s.py * 9277u + p.sampleIndex * 26699u) | 1u;
   float pixx = (float)(2 * s.px + 1) / (float)W - 1.0f;
   float pixy = (float)(2 * s.py + 1) / (float)H - 1.0f;
   float ax = (randf(s.seed) - 0.5f) / (float)W;
@@ -124,7 +124,7 @@ __device__ __forceinline__ bool continueFromHit(const RenderParams& p, PathState
     s.shC = (c * dot(N, L)) / pdf_light;
     shadow = true;
   }
-  const uint32_t gi = grayCode(p.frameCounter + 1u);
+  const uint32_t gi = grayCode(p.sampleIndex + 1u);
   float u = sobolf(2u * (uint32_t)nb, gi);
   float v = sobolf(2u * (uint32_t)nb + 1u, gi);
   cranleyPatterson(s.px, s.py, u, v);

@@ -107,7 +107,8 @@ int pt_create(pt_ctx** out, const pt_config* cfg) {
   if (!out || !cfg) return PT_E_INVALID;
   *out = nullptr;
   if (cfg->width <= 0 || cfg->height <= 0 || cfg->integrator < 0 || cfg->integrator > PT_BASIC_CPU_COMPAT ||
-      cfg->tile_world < 1 || cfg->tile_rank < 0 || cfg->tile_rank >= cfg->tile_world) {
+      cfg->tile_world < 1 || cfg->tile_rank < 0 || cfg->tile_rank >= cfg->tile_world || cfg->sample_world < 0 ||
+      cfg->sample_rank < 0 || cfg->sample_rank >= (cfg->sample_world > 0 ? cfg->sample_world : 1)) {
     g_create_err = "pt_create: invalid config";
     return PT_E_INVALID;
   }
@@ -342,6 +343,13 @@ static int launchEvents(pt_ctx* ctx, hipEvent_t* b, hipEvent_t* e) {
   return PT_OK;
 }
 
+// the RNG / Sobol sample index of frame frameCounter: sample-parallel ranks
+// interleave their sample streams (rank r renders samples r, r+W, r+2W, ...)
+static uint32_t sampleIndex(const pt_config& c, uint32_t frameCounter) {
+  const uint32_t w = c.sample_world > 0 ? (uint32_t)c.sample_world : 1u;
+  return frameCounter * w + (uint32_t)c.sample_rank;
+}
+
 static SceneView sceneView(const pt_ctx* ctx) {
   SceneView s;
   s.geo = ctx->d_geo;
@@ -441,6 +449,7 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
   p.width = c.width;
   p.height = c.height;
   p.frameCounter = frameCounter;
+  p.sampleIndex = sampleIndex(c, frameCounter);
   p.maxBounce = maxBounce;
   std::memcpy(p.eye, eye, sizeof(p.eye));
   std::memcpy(p.cam, cam, sizeof(p.cam));
@@ -496,7 +505,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
     p.nShapes = ctx->nShapes;
     p.width = c.width;
     p.height = c.height;
-    p.sample = frameCounter;
+    p.sample = sampleIndex(c, frameCounter);
     p.seed = c.basic_seed;
     p.maxDepth = c.max_bounce >= 0 ? c.max_bounce : 8;
     p.brightness = (float)((double)(2.0f * 3.1415926f) * (1.0 / (double)c.basic_samples));
@@ -535,6 +544,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   p.width = c.width;
   p.height = c.height;
   p.frameCounter = frameCounter;
+  p.sampleIndex = sampleIndex(c, frameCounter);
   p.maxBounce = c.max_bounce >= 0 ? c.max_bounce : defaultBounce(c.integrator);
   std::memcpy(p.eye, eye, sizeof(p.eye));
   std::memcpy(p.cam, cameraRotate, sizeof(p.cam));
@@ -604,7 +614,7 @@ int pt_download_accum(pt_ctx* ctx, float* accum) {
   if (!ctx || !accum) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
-  CK(hipMemcpyAsync(accum, ctx->d_accum, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipMemcpyAsync(accum, ctx->d_accum, bytes, hipMemcpyDefault, ctx->stream));  // host or device
   CK(hipStreamSynchronize(ctx->stream));
   return PT_OK;
 }
@@ -613,7 +623,7 @@ int pt_upload_accum(pt_ctx* ctx, const float* accum) {
   if (!ctx || !accum) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
-  CK(hipMemcpyAsync(ctx->d_accum, accum, bytes, hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_accum, accum, bytes, hipMemcpyDefault, ctx->stream));  // host or device
   CK(hipStreamSynchronize(ctx->stream));
   return PT_OK;
 }

@@ -60,7 +60,8 @@ struct WFParams {
   WFQueues q;
   float4* accum;
   int width, height;
-  uint32_t frameCounter;
+  uint32_t frameCounter;  // running-mean count
+  uint32_t sampleIndex;   // RNG / Sobol sample index
   int maxBounce;
   float eye[3];
   float cam[16];

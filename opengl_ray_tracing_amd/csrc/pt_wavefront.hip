@@ -85,7 +85,7 @@ __global__ __launch_bounds__(BLOCK) void wfGenKernel(WFParams p) {
   p.q.act[0][slot] = pid;
   if (!ok) return;
   const int W = p.width, H = p.height;
-  uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.frameCounter * 26699u) | 1u;
+  uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.sampleIndex * 26699u) | 1u;
   float pixx = (float)(2 * px + 1) / (float)W - 1.0f;
   float pixy = (float)(2 * py + 1) / (float)H - 1.0f;
   float ax = (randf(seed) - 0.5f) / (float)W;
@@ -263,7 +263,7 @@ __device__ __forceinline__ uint32_t prepareMIS(const WFParams& p, int pid, int p
     S.shD[pid] = f4(Ldir, 0.0f);
     cast |= WF_SHD;
   }
-  const uint32_t gi = grayCode(p.frameCounter + 1u);
+  const uint32_t gi = grayCode(p.sampleIndex + 1u);
   float u = sobolf(2u * (uint32_t)bounce, gi);
   float v = sobolf(2u * (uint32_t)bounce + 1u, gi);
   cranleyPatterson(px, py, u, v);

@@ -1,12 +1,19 @@
-"""Multi-GPU frame sharding: screen tiles of `shard` x `shard`
-pixels dealt round-robin over the ranks (tile t belongs to rank t % world),
-one process per GPU, one gather of the packed shards to rank 0 per presented
-frame over RCCL/xGMI.
+"""Multi-GPU rendering, one process per GPU. Two ways to split
+the per-pixel path:
 
-Every pixel's value depends only on (pixel, frameCounter) and its own running
-mean (pass1.fsh:73-76, :118-122, :868-871), so the reassembled frame is
-bit-identical to a single-GPU render. The packed order (tile, row, column)
-matches the kernels in csrc/pt_kernels.hip (packKernel / unpackKernel).
+* screen tiles (strong scaling): tiles of `shard` x `shard` pixels dealt
+  round-robin over the ranks (tile t belongs to rank t % world); one gather of
+  the packed shards to rank 0 per presented frame over RCCL/xGMI (FrameGather).
+  Every pixel's value depends only on (pixel, frameCounter) and its own running
+  mean (pass1.fsh:73-76, :118-122, :868-871), so the reassembled frame is
+  bit-identical to a single-GPU render. The packed order (tile, row, column)
+  matches the kernels in csrc/pt_kernels.hip (packKernel / unpackKernel).
+* sample streams (weak scaling): every rank renders the whole frame from its
+  own interleaved sample stream (pt_config.sample_rank / sample_world: rank r
+  draws samples r, r+W, r+2W, ...), with no collective per frame; the image is
+  the mean of the ranks' running means, combined by one RCCL reduce when it is
+  consumed (SampleReduce). Equal to the single-GPU mean over the same samples up
+  to float summation order.
 """
 from __future__ import annotations
 
@@ -79,7 +86,57 @@ class FrameGather:
 
     def __call__(self):
         self.r.pack_owned(self.send.data_ptr())
-        self.dist.gather(self.send, gather_list=self.recv, dst=0)
+        if _staged():  # gloo rehearsal: the collective on host copies
+            recv = [t.cpu() for t in self.recv] if self.rank == 0 else None
+            self.dist.gather(self.send.cpu(), gather_list=recv, dst=0)
+            if self.rank == 0:
+                for t, h in zip(self.recv, recv):
+                    t.copy_(h)
+        else:
+            self.dist.gather(self.send, gather_list=self.recv, dst=0)
         if self.rank == 0:
             for k in range(1, self.world):
                 self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
+
+
+def _staged() -> bool:
+    """True when the process group is gloo (CPU rehearsal of the RCCL path): device tensors
+    are staged through host copies around the collective."""
+    import torch.distributed as dist
+
+    return dist.get_backend() == "gloo"
+
+
+def combine_sample_means(img, rank: int, world: int):
+    """Mean over ranks of equally weighted running means (in place on rank 0's `img`)."""
+    import torch.distributed as dist
+
+    if img.is_cuda and _staged():
+        h = img.cpu()
+        dist.reduce(h, dst=0, op=dist.ReduceOp.SUM)
+        img.copy_(h)
+    else:
+        dist.reduce(img, dst=0, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        img.mul_(1.0 / world)
+    return img
+
+
+class SampleReduce:
+    """RCCL reduce of every rank's running mean (sample-parallel rendering) to rank 0.
+
+    The renderer's accumulation is copied (device to device, on the renderer's
+    stream = torch's current stream) into a torch buffer which is summed to rank
+    0 and scaled by 1/world; the ranks' own running means are left untouched.
+    """
+
+    def __init__(self, renderer, rank: int, world: int, device):
+        import torch
+
+        self.r, self.rank, self.world = renderer, rank, world
+        self.img = torch.empty((renderer.height, renderer.width, 4), dtype=torch.float32, device=device)
+        renderer.set_stream(torch.cuda.current_stream(device).cuda_stream)
+
+    def __call__(self):
+        self.r.accum_into(self.img.data_ptr())
+        return combine_sample_means(self.img, self.rank, self.world)

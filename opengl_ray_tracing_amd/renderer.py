@@ -58,7 +58,7 @@ def device_count() -> int:
 class Renderer:
     def __init__(self, width: int, height: int, integrator="lambert", max_bounce: int = -1, device: int = 0,
                  tile_rank: int = 0, tile_world: int = 1, tile_size: int = 32, flags: int = 0,
-                 basic_samples: int = 128, basic_seed: int = 0):
+                 basic_samples: int = 128, basic_seed: int = 0, sample_rank: int = 0, sample_world: int = 1):
         self._lib = _native.load()
         cfg = _native.PtConfig()
         cfg.width, cfg.height = int(width), int(height)
@@ -69,12 +69,14 @@ class Renderer:
         cfg.flags = int(flags)
         cfg.basic_samples = int(basic_samples)
         cfg.basic_seed = int(basic_seed) & 0xFFFFFFFF
+        cfg.sample_rank, cfg.sample_world = int(sample_rank), int(sample_world)
         h = C.c_void_p()
         _native.check(self._lib.pt_create(C.byref(h), C.byref(cfg)), None, "pt_create")
         self._h = h
         self.width, self.height = cfg.width, cfg.height
         self.integrator = cfg.integrator
         self.tile_rank, self.tile_world = cfg.tile_rank, cfg.tile_world
+        self.sample_rank, self.sample_world = cfg.sample_rank, cfg.sample_world
 
     def close(self):
         if getattr(self, "_h", None):
@@ -135,6 +137,11 @@ class Renderer:
         out = np.empty((self.height, self.width, 4), np.float32)
         self._ck(self._lib.pt_download_accum(self._h, _fp(out)), "pt_download_accum")
         return out
+
+    def accum_into(self, dptr: int):
+        """Copy the accumulation (H x W x 4 f32) into device memory at dptr (stream-ordered, synchronous)."""
+        self._ck(self._lib.pt_download_accum(self._h, C.cast(C.c_void_p(dptr), C.POINTER(C.c_float))),
+                 "pt_download_accum")
 
     def set_accum(self, a: np.ndarray):
         a = np.ascontiguousarray(a, np.float32).reshape(self.height, self.width, 4)

@@ -587,6 +587,12 @@ static v3 pt_disney_uniform(Ctx* cx, Hit hit, int maxBounce, uint32_t* seed) {
 }
 
 /* pathTracingImportanceSampling IS:761-841 */
+/* sample index of the frame: the reference's frameCounter unless sample-parallel */
+static inline uint32_t sample_index(const orc_frame* f) {
+  uint32_t w = f->sampleWorld > 0 ? (uint32_t)f->sampleWorld : 1u;
+  return f->frameCounter * w + (uint32_t)f->sampleRank;
+}
+
 static v3 pt_mis(Ctx* cx, Hit hit, int maxBounce, uint32_t* seed, int px, int py, uint32_t frameCounter) {
   const orc_scene* s = cx->s;
   v3 Lo = V3(0, 0, 0), history = V3(1, 1, 1);
@@ -649,7 +655,8 @@ static int default_bounce(int integrator) {
 /* main IS:844-872 (one pixel) */
 static void shade_gl_pixel(Ctx* cx, const orc_frame* f, int px, int py, float* accum) {
   const int W = f->width, H = f->height;
-  uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + f->frameCounter * 26699u) | 1u;
+  const uint32_t sidx = sample_index(f);
+  uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + sidx * 26699u) | 1u;
   float pixx = (float)(2 * px + 1) / (float)W - 1.0f;
   float pixy = (float)(2 * py + 1) / (float)H - 1.0f;
   float ax = (randf(&seed) - 0.5f) / (float)W;
@@ -670,7 +677,7 @@ static void shade_gl_pixel(Ctx* cx, const orc_frame* f, int px, int py, float* a
     v3 Li;
     if (f->integrator == ORC_LAMBERT_O) Li = pt_lambert(cx, first, mb, &seed);
     else if (f->integrator == ORC_DISNEY_UNIFORM_D) Li = pt_disney_uniform(cx, first, mb, &seed);
-    else Li = pt_mis(cx, first, mb, &seed, px, py, f->frameCounter);
+    else Li = pt_mis(cx, first, mb, &seed, px, py, sidx);
     color = add(Le, Li);
   }
   float* a = accum + 4 * ((size_t)py * W + px);
@@ -808,7 +815,7 @@ static v3 b_path(Ctx* cx, v3 S, v3 d, int maxDepth, uint32_t* seed) {
 /* pixel loop body B:366-430, one sample k = frameCounter */
 static void shade_basic_pixel(Ctx* cx, const orc_frame* f, int j, int i, float* accum) {
   const int W = f->width, H = f->height;
-  uint32_t k = f->frameCounter;
+  uint32_t k = sample_index(f);
   uint32_t seed = ((uint32_t)j * 1973u + (uint32_t)i * 9277u + k * 26699u + f->basicSeed * 0x9E3779B9u) | 1u;
   /* B:369-376: the screen coordinate is formed in double, then stored in a float vec3 */
   double xd = 2.0 * (double)j / (double)W - 1.0;

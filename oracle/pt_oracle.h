@@ -59,6 +59,8 @@ typedef struct orc_frame {
   float cameraRotate[16];   /* column-major (glm value_ptr order) */
   int basicSamples;         /* BASIC: SAMPLE (BasicRayTracingWithC++/main.cpp:17) */
   uint32_t basicSeed;       /* BASIC: per-run seed of the counter RNG */
+  int sampleRank, sampleWorld; /* RNG/Sobol sample = frameCounter*sampleWorld + sampleRank (0/0 = frameCounter);
+                                  the running-mean weight stays 1/(frameCounter+1) (pt_abi.h pt_config) */
 } orc_frame;
 
 typedef struct orc_counters {

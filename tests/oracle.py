@@ -27,7 +27,8 @@ class OrcScene(C.Structure):
 class OrcFrame(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("integrator", C.c_int), ("maxBounce", C.c_int),
                 ("frameCounter", C.c_uint32), ("eye", C.c_float * 3), ("cameraRotate", C.c_float * 16),
-                ("basicSamples", C.c_int), ("basicSeed", C.c_uint32)]
+                ("basicSamples", C.c_int), ("basicSeed", C.c_uint32), ("sampleRank", C.c_int),
+                ("sampleWorld", C.c_int)]
 
 
 class OrcCounters(C.Structure):
@@ -109,7 +110,7 @@ class Oracle:
         self.scene = s
 
     def render(self, width, height, integrator, frame, eye=None, rot=None, accum=None, pixels=None,
-               max_bounce=-1, threads=8, basic_samples=128, basic_seed=0):
+               max_bounce=-1, threads=8, basic_samples=128, basic_seed=0, sample_rank=0, sample_world=1):
         f = OrcFrame()
         f.width, f.height = width, height
         f.integrator = INTEG[integrator] if isinstance(integrator, str) else integrator
@@ -121,6 +122,7 @@ class Oracle:
             f.cameraRotate[:] = [float(x) for x in np.asarray(rot).reshape(16)]
         f.basicSamples = basic_samples
         f.basicSeed = basic_seed
+        f.sampleRank, f.sampleWorld = sample_rank, sample_world
         if accum is None:
             accum = np.zeros((height, width, 4), np.float32)
         assert accum.dtype == np.float32 and accum.flags.c_contiguous and accum.shape == (height, width, 4)

@@ -93,3 +93,52 @@ def test_gloo_gather_is_bit_exact(world):
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def _sample_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    import torch
+
+    import oracle
+    from opengl_ray_tracing_amd import orbit_camera, scenes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s = scenes.scene_c2()
+        s.build_bvh("sah", 8)
+        tris, nodes = s.encode()
+        env = scenes.synthetic_env(64, 32)
+        eye, rot = orbit_camera(0, 0, 4)
+        o = oracle.Oracle(tris, nodes, env)
+        frames = 2
+        acc = np.zeros((H, W, 4), np.float32)
+        for f in range(frames):  # this rank's samples: f * world + rank
+            acc, _ = o.render(W, H, "lambert", f, eye, rot, accum=acc, threads=1, sample_rank=rank,
+                              sample_world=world)
+        img = D.combine_sample_means(torch.from_numpy(acc.copy()), rank, world)
+        if rank == 0:
+            ref = np.zeros((H, W, 4), np.float32)
+            for f in range(frames * world):  # one rank, samples 0 .. frames*world-1
+                ref, _ = o.render(W, H, "lambert", f, eye, rot, accum=ref, threads=1)
+            got = img.numpy()
+            q.put(bool(np.allclose(got, ref, rtol=2e-5, atol=1e-6)) and bool(np.any(got != acc)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sample_parallel_mean(world):
+    """Sample-parallel ranks (interleaved sample streams, one reduce when the image is consumed)
+    give the single-rank running mean over the same samples, up to float summation order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sample_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
