@@ -14,7 +14,21 @@ constexpr int BLOCK = 256;        // 4 waves of 64
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
 constexpr int LDS_STACK = PT_LDS_STACK;  // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
-constexpr int NUM_QUEUES = 8;     // work counters, one per blockIdx % 8 group (XCD round-robin)
+#ifndef PT_NUM_QUEUES
+#define PT_NUM_QUEUES 32
+#endif
+// Device-scope atomics are serialised per cache line at the memory side (~88
+// same-line ops/us), so every hot counter lives on its own 256-byte line.
+constexpr int CTL_LINE_INTS = 64;
+constexpr int NUM_QUEUES = PT_NUM_QUEUES;  // work counters, queue q owned by blocks with blockIdx % NUM_QUEUES == q
+static_assert((NUM_QUEUES & (NUM_QUEUES - 1)) == 0 && NUM_QUEUES <= 64, "NUM_QUEUES: power of two <= 64");
+constexpr int RAY_SHARDS = 64;     // sharded ray counters (u64, one per 256-byte line)
+constexpr int RAY_SHARD_STRIDE = CTL_LINE_INTS / 2;  // in u64
+// control block layout (bytes)
+constexpr size_t CTL_QUEUES = 0;                                      // NUM_QUEUES padded int counters
+constexpr size_t CTL_STATS = 64 * 256;                                // 5 u64 cumulative fetch counters
+constexpr size_t CTL_RAYS = 65 * 256;                                 // RAY_SHARDS padded u64 counters
+constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;
 constexpr int MAX_LEAF = 1 << LEAF_CNT_BITS;
@@ -46,7 +60,7 @@ struct RenderParams {
   float eye[3];
   float cam[16];
   float4* accum;
-  int* queue;           // NUM_QUEUES counters, zeroed before each launch
+  int* queue;           // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
   int perQueue;         // items per queue
   int numItems;         // 8x8 wave tiles owned by this rank
   int shardSize;        // shard tile edge (multiple of 8)
@@ -56,7 +70,7 @@ struct RenderParams {
   int* ovf;             // traversal stack overflow (per thread ovfDepth ints), may be null
   int ovfDepth;
   unsigned long long* stats;  // [rays, nodes, tris, mats, texels]
-  unsigned long long* rayShards;  // 64 sharded ray counters (regen kernel)
+  unsigned long long* rayShards;  // RAY_SHARDS ray counters (stride RAY_SHARD_STRIDE)
 };
 
 struct TraceParams {

@@ -351,17 +351,10 @@ __global__ __launch_bounds__(BLOCK, PT_MIN_WAVES) void renderKernel(RenderParams
   const int home = blockIdx.x & (NUM_QUEUES - 1);
   const int tilesPerShard = p.shardTiles;  // 8x8 wave tiles per shard tile
   const int sub = p.shardSize >> 3;        // wave tiles per shard-tile edge
-  for (int qi = 0; qi < NUM_QUEUES;) {
-    const int q = (home + qi) & (NUM_QUEUES - 1);
-    int item = 0;
-    if (lane == 0) item = atomicAdd(p.queue + q, 1);
-    item = __shfl(item, 0, 64);
-    const int base = q * p.perQueue;
-    if (item >= p.perQueue || base + item >= p.numItems) {
-      qi++;
-      continue;
-    }
-    const int w = base + item;
+  int qi = 0;
+  while (true) {
+    const int w = nextTile(p.queue, p.perQueue, p.numItems, home, qi);
+    if (w < 0) break;
     const int j = w / tilesPerShard, s = w - j * tilesPerShard;
     const int g = j * p.world + p.rank;  // global shard tile id (row-major)
     const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
@@ -369,7 +362,7 @@ __global__ __launch_bounds__(BLOCK, PT_MIN_WAVES) void renderKernel(RenderParams
     const int py = gy * p.shardSize + (s / sub) * 8 + (lane >> 3);
     if (px < p.width && py < p.height) shadePixel<INTEG, CULL, COUNT>(p, px, py, st, C);
   }
-  uint32_t r = waveSum(C.rays);
+  addRays(p.rayShards, C.rays);
   if (COUNT) {
     uint32_t n = waveSum(C.nodes), t = waveSum(C.tris), m = waveSum(C.mats), x = waveSum(C.texels);
     if (lane == 0) {
@@ -379,7 +372,6 @@ __global__ __launch_bounds__(BLOCK, PT_MIN_WAVES) void renderKernel(RenderParams
       atomicAdd(reinterpret_cast<unsigned long long*>(p.stats + 4), (unsigned long long)x);
     }
   }
-  if (lane == 0 && r) atomicAdd(reinterpret_cast<unsigned long long*>(p.stats), (unsigned long long)r);
 }
 
 // ------------------------------------------------------------ batch query

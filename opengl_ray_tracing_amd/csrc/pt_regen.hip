@@ -242,18 +242,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
       const unsigned long long idle = __ballot(!active);
       if (idle == 0) break;
       if (cursor >= 64) {
-        int item = -1;
-        while (qi < NUM_QUEUES) {
-          const int q = (home + qi) & (NUM_QUEUES - 1);
-          int it = 0;
-          if (lane == 0) it = atomicAdd(p.queue + q, 1);
-          it = __shfl(it, 0, 64);
-          if (it < p.perQueue && q * p.perQueue + it < p.numItems) {
-            item = q * p.perQueue + it;
-            break;
-          }
-          qi++;
-        }
+        const int item = nextTile(p.queue, p.perQueue, p.numItems, home, qi);
         if (item < 0) break;  // no tiles left for this wave
         tile = item;
         cursor = 0;
@@ -284,9 +273,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
       active = false;
     }
   }
-  uint32_t r = C.rays;
-  for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
-  if (lane == 0 && r) atomicAdd(p.rayShards + (blockIdx.x & 63), (unsigned long long)r);
+  addRays(p.rayShards, C.rays);
 }
 
 template <int I>

@@ -22,8 +22,6 @@
 
 using namespace pt;
 
-static constexpr size_t CTL_RAY_SHARDS = 512;
-static constexpr size_t CTL_BYTES = CTL_RAY_SHARDS + WF_NSEG * sizeof(unsigned long long);
 
 struct pt_ctx {
   pt_config cfg{};
@@ -47,8 +45,8 @@ struct pt_ctx {
   int nShapes = 0;
   // frame state
   float4* d_accum = nullptr;
-  // [0,32) queue counters (zeroed per launch), [64,104) cumulative stats,
-  // [CTL_RAY_SHARDS, CTL_BYTES) WF_NSEG sharded cumulative ray counters
+  // control block (pt_kernels.h CTL_*): padded queue counters (zeroed per
+  // launch), cumulative fetch stats, padded sharded cumulative ray counters
   unsigned char* d_ctl = nullptr;
   int* d_ovf = nullptr;
   size_t ovfInts = 0;
@@ -374,6 +372,12 @@ static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDep
 }
 
 // ------------------------------------------------------------ wavefront pipeline
+// counter stages of the wavefront pipeline: gen + one per bounce + the last shade's output
+static int wfStages(const pt_ctx* ctx) {
+  const int mb = ctx->cfg.max_bounce >= 0 ? ctx->cfg.max_bounce : defaultBounce(ctx->cfg.integrator);
+  return std::min(mb, 250) + 2;
+}
+
 static int ensureWavefront(pt_ctx* ctx) {
   if (ctx->wfReady) return PT_OK;
   const size_t n = (size_t)ctx->cfg.width * ctx->cfg.height;
@@ -399,7 +403,7 @@ static int ensureWavefront(pt_ctx* ctx) {
     CK(hipMalloc(&ctx->wfq.cls[k], qn * sizeof(int)));
     CK(hipMalloc(&ctx->wfq.shd[k], qn * sizeof(int)));
   }
-  CK(hipMalloc(&ctx->wfq.cnt, (size_t)wfCnt(256, 0) * sizeof(int)));
+  CK(hipMalloc(&ctx->wfq.cnt, wfCnt(wfStages(ctx) + 1, 0) * sizeof(int)));
   ctx->wfReady = true;
   return PT_OK;
 }
@@ -420,7 +424,7 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
                            unsigned long long* stats, hipEvent_t evb, hipEvent_t eve) {
   const pt_config& c = ctx->cfg;
   (void)stats;
-  unsigned long long* rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAY_SHARDS);
+  unsigned long long* rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAYS);
   int rc = ensureWavefront(ctx);
   if (rc) return rc;
   const int maxBounce = c.max_bounce >= 0 ? c.max_bounce : defaultBounce(c.integrator);
@@ -458,7 +462,7 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
   p.shardsX = ctx->shardsX;
   p.rank = c.tile_rank;
   p.world = c.tile_world;
-  CK(hipMemsetAsync(ctx->wfq.cnt, 0, (size_t)wfCnt(maxBounce + 2, 0) * sizeof(int), ctx->stream));
+  CK(hipMemsetAsync(ctx->wfq.cnt, 0, wfCnt(maxBounce + 2, 0) * sizeof(int), ctx->stream));
   const int gridShade = segGrid(std::min<long>(((long)p.numOwned + BLOCK - 1) / BLOCK, (long)ctx->numCU * 16));
   CK(hipEventRecord(evb, ctx->stream));
   CK(wfLaunchGen(p, ctx->stream));
@@ -493,8 +497,8 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   const pt_config& c = ctx->cfg;
-  unsigned long long* stats = reinterpret_cast<unsigned long long*>(ctx->d_ctl + 64);
-  CK(hipMemsetAsync(ctx->d_ctl, 0, 32, ctx->stream));
+  unsigned long long* stats = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_STATS);
+  CK(hipMemsetAsync(ctx->d_ctl + CTL_QUEUES, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), ctx->stream));
   hipEvent_t evb, eve;
   int erc = launchEvents(ctx, &evb, &eve);
   if (erc) return erc;
@@ -560,7 +564,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   p.ovf = ovfDepth ? ctx->d_ovf : nullptr;
   p.ovfDepth = ovfDepth;
   p.stats = stats;
-  p.rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAY_SHARDS);
+  p.rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAYS);
   CK(hipEventRecord(evb, ctx->stream));
   if (regen) CK(launchRegen(p, c.integrator, grid, ctx->stream, cull));
   else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
@@ -705,12 +709,14 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   if (!ctx || !st) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
-  unsigned long long h[5], shards[WF_NSEG];
-  CK(hipMemcpy(h, ctx->d_ctl + 64, sizeof(h), hipMemcpyDeviceToHost));
-  CK(hipMemcpy(shards, ctx->d_ctl + CTL_RAY_SHARDS, sizeof(shards), hipMemcpyDeviceToHost));
+  unsigned long long h[5];
+  std::vector<unsigned long long> shards((size_t)RAY_SHARDS * RAY_SHARD_STRIDE);
+  CK(hipMemcpy(h, ctx->d_ctl + CTL_STATS, sizeof(h), hipMemcpyDeviceToHost));
+  CK(hipMemcpy(shards.data(), ctx->d_ctl + CTL_RAYS, shards.size() * sizeof(unsigned long long),
+               hipMemcpyDeviceToHost));
   std::memset(st, 0, sizeof(*st));
   st->rays = h[0];
-  for (int k = 0; k < WF_NSEG; k++) st->rays += shards[k];
+  for (int k = 0; k < RAY_SHARDS; k++) st->rays += shards[(size_t)k * RAY_SHARD_STRIDE];
   st->node_fetch = h[1];
   st->tri_fetch = h[2];
   st->mat_fetch = h[3];
@@ -771,7 +777,7 @@ int pt_reset_stats(pt_ctx* ctx) {
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
-  CK(hipMemset(ctx->d_ctl + 64, 0, CTL_BYTES - 64));
+  CK(hipMemset(ctx->d_ctl + CTL_STATS, 0, CTL_BYTES - CTL_STATS));
   ctx->launches = 0;
   return PT_OK;
 }

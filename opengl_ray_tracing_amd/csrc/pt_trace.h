@@ -196,6 +196,31 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
   return best;
 }
 
+// ----------------------------------------------------------------- work queue
+// Next 8x8 wave tile for the calling wave (wave-uniform result, -1 when every
+// queue is drained). Blocks start on their home queue (blockIdx % NUM_QUEUES;
+// consecutive block ids land on different XCDs) and then steal round-robin;
+// qi (wave-uniform) counts the queues found empty.
+__device__ __forceinline__ int nextTile(int* queue, int perQueue, int numItems, int home, int& qi) {
+  while (qi < NUM_QUEUES) {
+    const int q = (home + qi) & (NUM_QUEUES - 1);
+    int it = 0;
+    if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
+    it = __shfl(it, 0, 64);
+    const int item = q * perQueue + it;
+    if (it < perQueue && item < numItems) return item;
+    qi++;
+  }
+  return -1;
+}
+
+// per-wave sum of a lane counter into the block's padded shard
+__device__ __forceinline__ void addRays(unsigned long long* shards, uint32_t r) {
+  for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
+  if ((threadIdx.x & 63) == 0 && r)
+    atomicAdd(shards + (blockIdx.x & (RAY_SHARDS - 1)) * RAY_SHARD_STRIDE, (unsigned long long)r);
+}
+
 // The full HitResult (IS:63-71) of the winning triangle, computed once.
 struct Hit {
   V3 P, N, viewDir;

@@ -25,9 +25,12 @@ constexpr uint32_t WF_PRIMARY = 1u << 8;    // the closest-hit ray in flight is 
 constexpr uint32_t WF_CLS = 1u << 9;        // a closest-hit ray was cast
 constexpr uint32_t WF_SHD = 1u << 10;       // an env shadow ray was cast
 
-// counters: cnt[((stage * WF_CNT_TYPES) + type) * WF_NSEG + segment]
-constexpr int WF_CNT_ACT = 0, WF_CNT_CLS = 1, WF_CNT_SHD = 2, WF_CNT_TYPES = 4;
-__host__ __device__ constexpr int wfCnt(int stage, int type) { return (stage * WF_CNT_TYPES + type) * WF_NSEG; }
+// counters, each on its own 256-byte line (CTL_LINE_INTS):
+// cnt[(((stage * WF_CNT_TYPES) + type) * WF_NSEG + segment) * CTL_LINE_INTS]
+constexpr int WF_CNT_ACT = 0, WF_CNT_CLS = 1, WF_CNT_SHD = 2, WF_CNT_TYPES = 3;
+__host__ __device__ constexpr size_t wfCnt(int stage, int type, int seg = 0) {
+  return ((size_t)(stage * WF_CNT_TYPES + type) * WF_NSEG + seg) * CTL_LINE_INTS;
+}
 
 // path state, structure of arrays indexed by pixel id
 struct WFState {
@@ -72,7 +75,7 @@ struct WFParams {
 struct WFTraceParams {
   SceneView scene;
   const int* queue;   // segment s at queue + s * segCap
-  const int* count;   // WF_NSEG counters
+  const int* count;   // WF_NSEG counters, stride CTL_LINE_INTS
   int segCap;
   const float4* rayO;
   const float4* rayD;
@@ -80,7 +83,7 @@ struct WFTraceParams {
   int* occ;
   int* ovf;
   int ovfDepth;
-  unsigned long long* rays;  // WF_NSEG sharded ray counters
+  unsigned long long* rays;  // RAY_SHARDS padded ray counters
 };
 
 hipError_t wfLaunchGen(const WFParams& p, hipStream_t s);

@@ -25,18 +25,18 @@ namespace pt {
 // -------------------------------------------------------------- helpers
 __device__ __forceinline__ int laneId() { return threadIdx.x & 63; }
 
-// Append pred lanes' values to segment `seg` of queue q: one atomic per wave.
-__device__ __forceinline__ void waveAppend(int* q, int segCap, int* cnt, int seg, bool pred, int value) {
+// Append pred lanes' values to queue segment q (counter cnt): one atomic per wave.
+__device__ __forceinline__ void waveAppend(int* q, int* cnt, bool pred, int value) {
   unsigned long long m = __ballot(pred);
   if (m == 0) return;
   const int lane = laneId();
   const int leader = __ffsll((long long)m) - 1;
   int base = 0;
-  if (lane == leader) base = atomicAdd(cnt + seg, __popcll(m));
+  if (lane == leader) base = atomicAdd(cnt, __popcll(m));
   base = __shfl(base, leader, 64);
   if (pred) {
     unsigned long long below = m & ((1ull << lane) - 1ull);
-    q[seg * segCap + base + __popcll(below)] = value;
+    q[base + __popcll(below)] = value;
   }
 }
 
@@ -72,8 +72,8 @@ __global__ __launch_bounds__(BLOCK) void wfGenKernel(WFParams p) {
   if (blockIdx.x == 0 && threadIdx.x < WF_NSEG) {
     const int s = threadIdx.x;
     const int n = (tiles > s ? (tiles - s + WF_NSEG - 1) / WF_NSEG : 0) * 64;
-    p.q.cnt[wfCnt(0, WF_CNT_CLS) + s] = n;
-    p.q.cnt[wfCnt(0, WF_CNT_ACT) + s] = n;
+    p.q.cnt[wfCnt(0, WF_CNT_CLS, s)] = n;
+    p.q.cnt[wfCnt(0, WF_CNT_ACT, s)] = n;
   }
   if (k >= p.numOwned) return;
   int px = 0, py = 0;
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(BLOCK) void wfTraceKernel(WFTraceParams p) {
   st.gbl = p.ovf ? p.ovf + gtid * p.ovfDepth : nullptr;
   st.sp = 0;
   const int seg = blockIdx.x & (WF_NSEG - 1);
-  const int n = p.count[seg];
+  const int n = p.count[seg * CTL_LINE_INTS];
   const int* q = p.queue + (size_t)seg * p.segCap;
   const int stride = (gridDim.x / WF_NSEG) * BLOCK;
   int next = (blockIdx.x / WF_NSEG) * BLOCK + threadIdx.x;
@@ -213,8 +213,7 @@ __global__ __launch_bounds__(BLOCK) void wfTraceKernel(WFTraceParams p) {
     }
   }
   // per-wave ray count into the block's counter shard
-  for (int off = 32; off > 0; off >>= 1) nrays += __shfl_down(nrays, off, 64);
-  if (laneId() == 0 && nrays) atomicAdd(p.rays + seg, (unsigned long long)nrays);
+  addRays(p.rays, nrays);
 }
 
 // -------------------------------------------------------------- shade
@@ -290,9 +289,9 @@ template <int INTEG>
 __global__ __launch_bounds__(BLOCK) void wfShadeKernel(WFParams p, int stage) {
   const int in = stage & 1, out = in ^ 1;
   const int seg = blockIdx.x & (WF_NSEG - 1);
-  const int n = p.q.cnt[wfCnt(stage, WF_CNT_ACT) + seg];
+  const int n = p.q.cnt[wfCnt(stage, WF_CNT_ACT, seg)];
   const int* qin = p.q.act[in] + (size_t)seg * p.q.segCap;
-  int* cntOut = p.q.cnt + wfCnt(stage + 1, 0);
+
   const WFState& S = p.st;
   const int stride = (gridDim.x / WF_NSEG) * BLOCK;
   const int waveBase = (blockIdx.x / WF_NSEG) * BLOCK + (threadIdx.x & ~63);
@@ -403,9 +402,9 @@ __global__ __launch_bounds__(BLOCK) void wfShadeKernel(WFParams p, int stage) {
         S.Lo[pid] = f4(Lo, 0.0f);
       }
     }
-    waveAppend(p.q.cls[out], p.q.segCap, cntOut + WF_CNT_CLS * WF_NSEG, seg, toCls, pid);
-    waveAppend(p.q.shd[out], p.q.segCap, cntOut + WF_CNT_SHD * WF_NSEG, seg, toShd, pid);
-    waveAppend(p.q.act[out], p.q.segCap, cntOut + WF_CNT_ACT * WF_NSEG, seg, toAct, pid);
+    waveAppend(p.q.cls[out] + (size_t)seg * p.q.segCap, p.q.cnt + wfCnt(stage + 1, WF_CNT_CLS, seg), toCls, pid);
+    waveAppend(p.q.shd[out] + (size_t)seg * p.q.segCap, p.q.cnt + wfCnt(stage + 1, WF_CNT_SHD, seg), toShd, pid);
+    waveAppend(p.q.act[out] + (size_t)seg * p.q.segCap, p.q.cnt + wfCnt(stage + 1, WF_CNT_ACT, seg), toAct, pid);
   }
 }
 
