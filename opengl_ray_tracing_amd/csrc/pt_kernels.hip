@@ -351,9 +351,9 @@ __global__ __launch_bounds__(BLOCK, PT_MIN_WAVES) void renderKernel(RenderParams
   const int home = blockIdx.x & (NUM_QUEUES - 1);
   const int tilesPerShard = p.shardTiles;  // 8x8 wave tiles per shard tile
   const int sub = p.shardSize >> 3;        // wave tiles per shard-tile edge
-  int qi = 0;
+  TileCursor cur;
   while (true) {
-    const int w = nextTile(p.queue, p.perQueue, p.numItems, home, qi);
+    const int w = cur.next(p.queue, p.perQueue, p.numItems, home);
     if (w < 0) break;
     const int j = w / tilesPerShard, s = w - j * tilesPerShard;
     const int g = j * p.world + p.rank;  // global shard tile id (row-major)

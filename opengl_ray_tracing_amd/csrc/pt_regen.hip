@@ -229,7 +229,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
   const unsigned long long below = (1ull << lane) - 1ull;
   const int home = blockIdx.x & (NUM_QUEUES - 1);
   const int sub = p.shardSize >> 3;
-  int qi = 0;         // queues tried (wave-uniform)
+  TileCursor cur;     // wave-uniform
   int tile = -1;      // current 8x8 wave tile (wave-uniform)
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
   bool active = false;
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
       const unsigned long long idle = __ballot(!active);
       if (idle == 0) break;
       if (cursor >= 64) {
-        const int item = nextTile(p.queue, p.perQueue, p.numItems, home, qi);
+        const int item = cur.next(p.queue, p.perQueue, p.numItems, home);
         if (item < 0) break;  // no tiles left for this wave
         tile = item;
         cursor = 0;

@@ -197,22 +197,29 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
 }
 
 // ----------------------------------------------------------------- work queue
-// Next 8x8 wave tile for the calling wave (wave-uniform result, -1 when every
-// queue is drained). Blocks start on their home queue (blockIdx % NUM_QUEUES;
-// consecutive block ids land on different XCDs) and then steal round-robin;
-// qi (wave-uniform) counts the queues found empty.
-__device__ __forceinline__ int nextTile(int* queue, int perQueue, int numItems, int home, int& qi) {
-  while (qi < NUM_QUEUES) {
-    const int q = (home + qi) & (NUM_QUEUES - 1);
-    int it = 0;
-    if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
-    it = __shfl(it, 0, 64);
-    const int item = q * perQueue + it;
-    if (it < perQueue && item < numItems) return item;
-    qi++;
+// The next 8x8 wave tile for the calling wave (wave-uniform; -1 when every queue is
+// drained). Queue q holds tiles [q*perQueue, (q+1)*perQueue): one contiguous
+// band of the frame, served first by the blocks with blockIdx % NUM_QUEUES == q
+// (and so by one XCD under round-robin block placement), which keeps a band's
+// BVH and env-map lines in that XCD's L2; after its home queue a wave steals
+// round-robin. One tile per atomic measured best:
+// claiming 2 or 4 per atomic, interleaving the queues or grouping an XCD's
+// queues into one band were all slower or neutral.
+struct TileCursor {
+  int qi = 0;  // queues found empty (wave-uniform)
+  __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home) {
+    while (qi < NUM_QUEUES) {
+      const int q = (home + qi) & (NUM_QUEUES - 1);
+      int it = 0;
+      if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
+      it = __shfl(it, 0, 64);
+      const int t = q * perQueue + it;
+      if (it < perQueue && t < numItems) return t;
+      qi++;
+    }
+    return -1;
   }
-  return -1;
-}
+};
 
 // per-wave sum of a lane counter into the block's padded shard
 __device__ __forceinline__ void addRays(unsigned long long* shards, uint32_t r) {
