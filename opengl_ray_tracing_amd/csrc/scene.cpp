@@ -719,11 +719,6 @@ bool decrunch(RGBE* scanline, int len, Reader& f) {
   }
   return !f.eof;
 }
-float convertComponent(int expo, int val) {
-  float v = val / 256.0f;
-  float d = (float)std::pow(2.0, (double)expo);
-  return v * d;
-}
 }  // namespace
 
 int pt_hdr_decode(const unsigned char* bytes, int64_t nbytes, int* w_out, int* h_out, float** cols_out) {
@@ -752,14 +747,18 @@ int pt_hdr_decode(const unsigned char* bytes, int64_t nbytes, int* w_out, int* h
   if (!cols) return -5;
   std::vector<unsigned char> scan((size_t)w * 4);
   RGBE* scanline = reinterpret_cast<RGBE*>(scan.data());
+  // convertComponent (hdrloader.cpp:99-104) = val/256 * (float)pow(2, expo):
+  // the 256 possible scale factors are tabulated with the same expression
+  float scale[256];
+  for (int e = 0; e < 256; e++) scale[e] = (float)std::pow(2.0, (double)(e - 128));
   float* out = cols;
   for (int y = h - 1; y >= 0; y--) {
     if (!decrunch(scanline, w, f)) break;
     for (int k = 0; k < w; k++) {
-      int expo = scanline[k][3] - 128;
-      out[3 * k] = convertComponent(expo, scanline[k][0]);
-      out[3 * k + 1] = convertComponent(expo, scanline[k][1]);
-      out[3 * k + 2] = convertComponent(expo, scanline[k][2]);
+      const float d = scale[scanline[k][3]];
+      out[3 * k] = (scanline[k][0] / 256.0f) * d;
+      out[3 * k + 1] = (scanline[k][1] / 256.0f) * d;
+      out[3 * k + 2] = (scanline[k][2] / 256.0f) * d;
     }
     out += (size_t)w * 3;
   }
