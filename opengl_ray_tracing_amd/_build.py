@@ -31,7 +31,7 @@ HIP_FLAGS = [
     "-ffp-contract=off",
     "-Wall", "-Wno-unused-function",
 ]
-CXX_FLAGS = ["-O2", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+CXX_FLAGS = ["-O2", "-fPIC", "-pthread", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall",
              "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"]
 
 SOURCES = {
@@ -82,7 +82,7 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
                 if verbose and (r.stdout or r.stderr):
                     sys.stderr.write(r.stdout + r.stderr)
     if force or jobs or _stale(LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(LIB), *map(str, objs)])
     return LIB
 
 
@@ -109,7 +109,7 @@ def build_variant(name: str, defines: dict) -> Path:
         else:
             _run(["g++", *CXX_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
     lib = variant_lib(name)
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(lib), *map(str, objs)])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(lib), *map(str, objs)])
     return lib
 
 

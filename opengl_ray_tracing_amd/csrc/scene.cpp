@@ -13,6 +13,7 @@
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -195,41 +196,20 @@ int new_node(std::vector<BVHNode>& nodes) {
   return id;
 }
 
-// buildBVH (main.cpp:376-427)
-int buildBVH(std::vector<Triangle>& tr, std::vector<BVHNode>& nodes, int l, int r, int n) {
-  if (l > r) return 0;
-  int id = new_node(nodes);
-  node_bounds(tr, l, r, nodes[id]);
-  if ((r - l + 1) <= n) {
-    nodes[id].n = r - l + 1;
-    nodes[id].index = l;
-    return id;
-  }
-  float lenx = nodes[id].BB.x - nodes[id].AA.x;
-  float leny = nodes[id].BB.y - nodes[id].AA.y;
-  float lenz = nodes[id].BB.z - nodes[id].AA.z;
+// buildBVH (main.cpp:376-427): split at the median of the longest axis.
+int splitMedian(std::vector<Triangle>& tr, const BVHNode& node, int l, int r, bool) {
+  float lenx = node.BB.x - node.AA.x;
+  float leny = node.BB.y - node.AA.y;
+  float lenz = node.BB.z - node.AA.z;
   if (lenx >= leny && lenx >= lenz) std::sort(tr.begin() + l, tr.begin() + r + 1, CmpAxis{0});
   if (leny >= lenx && leny >= lenz) std::sort(tr.begin() + l, tr.begin() + r + 1, CmpAxis{1});
   if (lenz >= lenx && lenz >= leny) std::sort(tr.begin() + l, tr.begin() + r + 1, CmpAxis{2});
-  int mid = (l + r) / 2;
-  int left = buildBVH(tr, nodes, l, mid, n);
-  int right = buildBVH(tr, nodes, mid + 1, r, n);
-  nodes[id].left = left;
-  nodes[id].right = right;
-  return id;
+  return (l + r) / 2;
 }
 
 // buildBVHwithSAH (main.cpp:430-551). zTypo reproduces main.cpp:480,484
 // (t.p2.x in the z prefix bounds).
-int buildSAH(std::vector<Triangle>& tr, std::vector<BVHNode>& nodes, int l, int r, int n, bool zTypo) {
-  if (l > r) return 0;
-  int id = new_node(nodes);
-  node_bounds(tr, l, r, nodes[id]);
-  if ((r - l + 1) <= n) {
-    nodes[id].n = r - l + 1;
-    nodes[id].index = l;
-    return id;
-  }
+int splitSAH(std::vector<Triangle>& tr, const BVHNode&, int l, int r, bool zTypo) {
   float Cost = kINF;
   int Axis = 0;
   int Split = (l + r) / 2;
@@ -296,14 +276,7 @@ int buildSAH(std::vector<Triangle>& tr, std::vector<BVHNode>& nodes, int l, int 
     }
   }
   std::sort(&tr[0] + l, &tr[0] + r + 1, CmpAxis{Axis});
-  // free the prefix arrays before recursing (the reference keeps them alive: memory only)
-  std::vector<f3>().swap(leftMax); std::vector<f3>().swap(leftMin);
-  std::vector<f3>().swap(rightMax); std::vector<f3>().swap(rightMin);
-  int left = buildSAH(tr, nodes, l, Split, n, zTypo);
-  int right = buildSAH(tr, nodes, Split + 1, r, n, zTypo);
-  nodes[id].left = left;
-  nodes[id].right = right;
-  return id;
+  return Split;  // the prefix arrays are freed before recursing (the reference keeps them: memory only)
 }
 
 // Binned SAH (32 bins over centroid bounds), O(n log n). Not a reference
@@ -327,16 +300,7 @@ inline float area(const Box& b) {
   f3 d = b.hi - b.lo;
   return 2.0f * (d.x * d.y + d.x * d.z + d.y * d.z);
 }
-int buildBinned(std::vector<Triangle>& tr, std::vector<BVHNode>& nodes, int l, int r, int n) {
-  if (l > r) return 0;
-  int id = new_node(nodes);
-  node_bounds(tr, l, r, nodes[id]);
-  const int cnt = r - l + 1;
-  if (cnt <= n) {
-    nodes[id].n = cnt;
-    nodes[id].index = l;
-    return id;
-  }
+int splitBinned(std::vector<Triangle>& tr, const BVHNode&, int l, int r, bool) {
   Box cb = empty_box();
   for (int i = l; i <= r; i++) grow(cb, F3(centre(tr[i], 0), centre(tr[i], 1), centre(tr[i], 2)));
   const int NB = 32;
@@ -385,12 +349,59 @@ int buildBinned(std::vector<Triangle>& tr, std::vector<BVHNode>& nodes, int l, i
     mid = (int)(it - tr.begin()) - 1;
     if (mid < l || mid >= r) mid = (l + r) / 2;
   }
-  int left = buildBinned(tr, nodes, l, mid, n);
-  int right = buildBinned(tr, nodes, mid + 1, r, n);
+  return mid;
+}
+
+// Recursive build shared by the builders: preorder node ids (a node, then its
+// left subtree, then its right subtree), contiguous leaf ranges. Subtrees of
+// more than kParMin triangles are built on their own threads (up to parDepth
+// levels deep) into private arrays that are spliced back in preorder, so the
+// node array and the triangle order are identical to a serial build.
+typedef int (*SplitFn)(std::vector<Triangle>&, const BVHNode&, int, int, bool);
+constexpr int kParMin = 8192;
+
+int splice(std::vector<BVHNode>& nodes, const std::vector<BVHNode>& local, int root) {
+  if (root == 0) return 0;
+  const int shift = (int)nodes.size() - 1;  // local ids start at 1 (slot 0 is a placeholder)
+  for (size_t k = 1; k < local.size(); k++) {
+    BVHNode x = local[k];
+    if (x.left > 0) x.left += shift;
+    if (x.right > 0) x.right += shift;
+    nodes.push_back(x);
+  }
+  return root + shift;
+}
+
+int buildTree(std::vector<Triangle>& tr, std::vector<BVHNode>& nodes, int l, int r, int n, SplitFn split, bool flag,
+              int parDepth) {
+  if (l > r) return 0;
+  const int id = new_node(nodes);
+  node_bounds(tr, l, r, nodes[id]);
+  if ((r - l + 1) <= n) {
+    nodes[id].n = r - l + 1;
+    nodes[id].index = l;
+    return id;
+  }
+  const int mid = split(tr, nodes[id], l, r, flag);
+  int left, right;
+  if (parDepth > 0 && r - l + 1 >= kParMin) {
+    std::vector<BVHNode> ln(1), rn(1);
+    int lr = 0;
+    std::thread th([&] { lr = buildTree(tr, ln, l, mid, n, split, flag, parDepth - 1); });
+    const int rr = buildTree(tr, rn, mid + 1, r, n, split, flag, parDepth - 1);
+    th.join();
+    left = splice(nodes, ln, lr);
+    right = splice(nodes, rn, rr);
+  } else {
+    left = buildTree(tr, nodes, l, mid, n, split, flag, 0);
+    right = buildTree(tr, nodes, mid + 1, r, n, split, flag, 0);
+  }
   nodes[id].left = left;
   nodes[id].right = right;
   return id;
 }
+
+
 
 int tree_depth(const std::vector<BVHNode>& nodes) {
   if (nodes.size() < 2) return 0;
@@ -573,11 +584,15 @@ int pt_scene_build_bvh(pt_scene* s, int builder, int leafSize) {
   s->nodes.assign(1, testNode);
   s->nodes.reserve(2 * s->triangles.size() / (size_t)leafSize + 16);
   int r = (int)s->triangles.size() - 1;
+  // threads: up to 2^parDepth subtrees in flight
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  int parDepth = 0;
+  while ((1u << parDepth) < hw) parDepth++;
   switch (builder) {
-    case PT_BVH_REFERENCE_SAH: buildSAH(s->triangles, s->nodes, 0, r, leafSize, true); break;
-    case PT_BVH_REFERENCE_MEDIAN: buildBVH(s->triangles, s->nodes, 0, r, leafSize); break;
-    case PT_BVH_FIXED_SAH: buildSAH(s->triangles, s->nodes, 0, r, leafSize, false); break;
-    case PT_BVH_BINNED_SAH: buildBinned(s->triangles, s->nodes, 0, r, leafSize); break;
+    case PT_BVH_REFERENCE_SAH: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitSAH, true, parDepth); break;
+    case PT_BVH_REFERENCE_MEDIAN: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitMedian, false, parDepth); break;
+    case PT_BVH_FIXED_SAH: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitSAH, false, parDepth); break;
+    case PT_BVH_BINNED_SAH: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitBinned, false, parDepth); break;
     default: return -1;
   }
   s->depth = tree_depth(s->nodes);

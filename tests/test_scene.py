@@ -165,3 +165,27 @@ def test_cornell_shapes():
     assert np.sum(sh[:, 16] == 1) == 2  # emissive light triangles
     tri = sh[sh[:, 0] == 0]
     assert np.allclose(np.linalg.norm(tri[:, 13:16], axis=1), 1, atol=1e-6)
+
+
+# sha1 of encode() for a 39,762-triangle heightfield, produced by the serial
+# (single-threaded) builders before the threaded build existed: subtrees above
+# 8,192 triangles are now built on their own threads and spliced back in
+# preorder, which must not change a single bit of the arrays.
+SERIAL_BUILD_SHA1 = {
+    "median": "90c51138bb41f6d860d12280873309b00ed61797",
+    "fixed_sah": "9fd2b6ece29ee6806aa6321cffbf93c8092a5ee4",
+    "binned": "61b7d43dc35f341155d574a9e3562cb1f277715e",
+}
+
+
+@pytest.mark.parametrize("builder", sorted(SERIAL_BUILD_SHA1))
+def test_threaded_build_equals_serial_build(builder):
+    import hashlib
+    from opengl_ray_tracing_amd.scene import Material, Scene
+    v, i = scenes.heightfield(142)
+    s = Scene()
+    s.add_mesh(v, i, Material())
+    s.build_bvh(builder, 8)
+    t, n = s.encode()
+    check_tree(t, n, 8)
+    assert hashlib.sha1(t.tobytes() + n.tobytes()).hexdigest() == SERIAL_BUILD_SHA1[builder]
