@@ -70,6 +70,18 @@ int pt_hdr_cache(const float* hdr, int w, int h, float* cache_out);
 /* BASIC_CPU_COMPAT shape records (24 f32 each, see oracle/pt_oracle.h). */
 #define PT_SHAPE_FLOATS 24
 
+/* Image output. The GL demos only display; BasicRayTracingWithC++ writes its
+ * image with imshow + svpng (main.cpp:169-190). pixels: h rows of w pixels of
+ * `channels` (3 or 4; alpha is dropped) f32, row 0 first.
+ * PFM ("PF", little-endian): linear values, rows written in stored order, which
+ * PFM reads bottom-to-top -- the accumulation's row 0 is the bottom (GL).
+ * PNG (8-bit RGB, uncompressed deflate like svpng): each component
+ * (unsigned char)clamp(pow(v, 1/gamma) * 255, 0, 255) in double as imshow does
+ * (gamma <= 0: no gamma); flip_rows writes the last row first (GL -> image). */
+int pt_image_write_pfm(const char* path, const float* pixels, int w, int h, int channels);
+int pt_image_write_png(const char* path, const float* pixels, int w, int h, int channels, float gamma,
+                       int flip_rows);
+
 #ifdef __cplusplus
 }
 #endif

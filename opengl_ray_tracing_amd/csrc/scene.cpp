@@ -797,6 +797,102 @@ int pt_hdr_load(const char* path, int* w, int* h, float** cols) {
 
 void pt_free(void* p) { std::free(p); }
 
+int pt_image_write_pfm(const char* path, const float* px, int w, int h, int channels) {
+  if (!path || !px || w <= 0 || h <= 0 || (channels != 3 && channels != 4)) return -1;
+  FILE* fp = std::fopen(path, "wb");
+  if (!fp) return -6;
+  std::fprintf(fp, "PF\n%d %d\n-1.0\n", w, h);
+  std::vector<float> row((size_t)w * 3);
+  bool ok = true;
+  for (int y = 0; y < h && ok; y++) {
+    const float* src = px + (size_t)y * w * channels;
+    for (int x = 0; x < w; x++)
+      for (int c = 0; c < 3; c++) row[(size_t)x * 3 + c] = src[(size_t)x * channels + c];
+    ok = std::fwrite(row.data(), sizeof(float), row.size(), fp) == row.size();
+  }
+  return (std::fclose(fp) == 0 && ok) ? 0 : -6;
+}
+
+namespace {
+uint32_t crc32_update(uint32_t crc, const unsigned char* p, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  for (size_t i = 0; i < n; i++) crc = table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+  return crc;
+}
+void put_be32(std::vector<unsigned char>& v, uint32_t x) {
+  v.push_back((unsigned char)(x >> 24)); v.push_back((unsigned char)(x >> 16));
+  v.push_back((unsigned char)(x >> 8)); v.push_back((unsigned char)x);
+}
+void png_chunk(std::vector<unsigned char>& out, const char* type, const std::vector<unsigned char>& data) {
+  put_be32(out, (uint32_t)data.size());
+  const size_t start = out.size();
+  out.insert(out.end(), type, type + 4);
+  out.insert(out.end(), data.begin(), data.end());
+  put_be32(out, crc32_update(0xffffffffu, out.data() + start, out.size() - start) ^ 0xffffffffu);
+}
+}  // namespace
+
+int pt_image_write_png(const char* path, const float* px, int w, int h, int channels, float gamma, int flip_rows) {
+  if (!path || !px || w <= 0 || h <= 0 || (channels != 3 && channels != 4) || w > (1 << 24)) return -1;
+  // raw scanlines: filter byte 0 + RGB
+  const size_t stride = (size_t)w * 3 + 1;
+  std::vector<unsigned char> raw(stride * h);
+  const double e = gamma > 0.0f ? (double)(1.0f / gamma) : 1.0;  // imshow: pow(double, 1.0f / 2.2f)
+  for (int y = 0; y < h; y++) {
+    const int sy = flip_rows ? h - 1 - y : y;
+    const float* src = px + (size_t)sy * w * channels;
+    unsigned char* dst = raw.data() + (size_t)y * stride;
+    *dst++ = 0;
+    for (int x = 0; x < w; x++)
+      for (int c = 0; c < 3; c++) {
+        double v = (double)src[(size_t)x * channels + c];
+        double g = gamma > 0.0f ? std::pow(v, e) * 255.0 : v * 255.0;
+        g = g < 0.0 ? 0.0 : (g > 255.0 ? 255.0 : g);  // clamp (NaN stays NaN -> 0 below)
+        *dst++ = (unsigned char)(g == g ? g : 0.0);
+      }
+  }
+  // zlib stream of stored deflate blocks (<= 65535 bytes each) + adler32
+  std::vector<unsigned char> z = {0x78, 0x01};
+  uint32_t a = 1, b = 0;
+  for (size_t off = 0; off < raw.size() || raw.empty();) {
+    const size_t n = std::min<size_t>(65535, raw.size() - off);
+    const bool last = off + n >= raw.size();
+    z.push_back(last ? 1 : 0);
+    z.push_back((unsigned char)(n & 0xff)); z.push_back((unsigned char)(n >> 8));
+    z.push_back((unsigned char)(~n & 0xff)); z.push_back((unsigned char)((~n >> 8) & 0xff));
+    for (size_t i = 0; i < n; i++) {
+      const unsigned char c = raw[off + i];
+      z.push_back(c);
+      a = (a + c) % 65521u;
+      b = (b + a) % 65521u;
+    }
+    off += n;
+    if (last) break;
+  }
+  put_be32(z, (b << 16) | a);
+  std::vector<unsigned char> out = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+  std::vector<unsigned char> ihdr;
+  put_be32(ihdr, (uint32_t)w);
+  put_be32(ihdr, (uint32_t)h);
+  ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});  // 8-bit RGB, deflate, no filter, no interlace
+  png_chunk(out, "IHDR", ihdr);
+  png_chunk(out, "IDAT", z);
+  png_chunk(out, "IEND", {});
+  FILE* fp = std::fopen(path, "wb");
+  if (!fp) return -6;
+  const bool ok = std::fwrite(out.data(), 1, out.size(), fp) == out.size();
+  return (std::fclose(fp) == 0 && ok) ? 0 : -6;
+}
+
 // calculateHdrCache (ImportanceSampling_LowDiscrepancySequence/main.cpp:555-652)
 int pt_hdr_cache(const float* HDR, int width, int height, float* cache) {
   if (!HDR || !cache || width <= 0 || height <= 0) return -1;

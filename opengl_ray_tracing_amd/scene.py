@@ -174,3 +174,31 @@ def calculate_hdr_cache(hdr: np.ndarray) -> np.ndarray:
     out = np.zeros((h, w, 3), np.float32)
     _native.check(lib.pt_hdr_cache(_fp(hdr), w, h, _fp(out)), None, "calculate_hdr_cache")
     return out
+
+
+def write_pfm(path: str, img: np.ndarray) -> None:
+    """Linear (h, w, 3|4) f32 image as PFM; row 0 is the bottom (the accumulation's GL order)."""
+    lib = _native.load()
+    img = np.ascontiguousarray(img, np.float32)
+    h, w, c = img.shape
+    _native.check(lib.pt_image_write_pfm(str(path).encode(), _fp(img), w, h, c), None, f"write_pfm({path})")
+
+
+def write_png(path: str, img: np.ndarray, gamma: float = 2.2, flip_rows: bool = True) -> None:
+    """8-bit RGB PNG as BasicRayTracingWithC++'s imshow (main.cpp:169-190): clamp(pow(v, 1/gamma)*255).
+    flip_rows: the accumulation's row 0 is the bottom; the BASIC integrator's is the top (pass False)."""
+    lib = _native.load()
+    img = np.ascontiguousarray(img, np.float32)
+    h, w, c = img.shape
+    _native.check(lib.pt_image_write_png(str(path).encode(), _fp(img), w, h, c, float(gamma), int(flip_rows)),
+                  None, f"write_png({path})")
+
+
+def read_pfm(path: str) -> np.ndarray:
+    """(h, w, 3) f32 in stored row order (PFM rows run bottom to top)."""
+    with open(path, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = map(int, f.readline().split())
+        scale = float(f.readline())
+        data = np.frombuffer(f.read(), "<f4" if scale < 0 else ">f4", count=w * h * 3)
+    return data.reshape(h, w, 3).astype(np.float32)
