@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--builder", default=None, help="override the config's BVH builder")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-psnr", action="store_true", help="skip the spp-matched PSNR check")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="cpu_baseline sample: full frames are rendered until this much CPU wall time has passed")
     ap.add_argument("--traffic", default=str(ROOT / "profiles" / "r1" / "traffic.json"),
@@ -177,6 +178,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and n == 1:
             cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_seconds)
+        quality = spp_matched_psnr(local) if not args.no_psnr else None
         line = {
             "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
@@ -190,7 +192,7 @@ def main():
                        if args.shard == "tiles" else
                        (f"sample-parallel x{n}" + (" (RCCL reduce of the running means after the run)"
                                                    if n > 1 else ""))},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "cpu_baseline": cpu, "quality": quality,
         }
         if combined_finite is not None:
             line["config"]["combined_image_finite"] = combined_finite
@@ -198,6 +200,36 @@ def main():
     r.close()
     if n > 1:
         dist.destroy_process_group()
+
+
+REF_PSNR_128SPP = 20.71  # the reference CPU tracer at 128 spp vs its 4000spp.png
+
+
+def spp_matched_psnr(device: int, spp: int = 128):
+    """The metric's "CPU-ref spp-matched PSNR": the BasicRayTracingWithC++ scene (config c1, 256x256)
+    rendered by the GPU BASIC_CPU_COMPAT integrator at 128 spp, imshow'd (main.cpp:169-190) and
+    compared with the reference's own 4000 spp image; the reference at 128 spp scores 20.71 dB."""
+    from PIL import Image
+
+    from opengl_ray_tracing_amd import Renderer, scenes
+    gold = ROOT / "tests" / "golden" / "4000spp.png"
+    if not gold.exists():
+        return None
+    with Renderer(256, 256, "basic", basic_samples=spp, device=device) as r:
+        r.upload_shapes(scenes.cornell_shapes())
+        z, eye4 = np.zeros(3, np.float32), np.eye(4, dtype=np.float32)
+        t0 = time.perf_counter()
+        for k in range(spp):
+            r.render_frame(z, eye4, k, sync=False)
+        r.synchronize()
+        dt = time.perf_counter() - t0
+        acc = r.accum()
+    img = np.clip(np.power(np.maximum(acc[..., :3].astype(np.float64), 0), 1 / 2.2) * 255, 0, 255).astype(np.uint8)
+    ref = np.asarray(Image.open(gold))[..., :3].astype(np.float64)
+    psnr = 10 * np.log10(255.0 ** 2 / np.mean((img.astype(np.float64) - ref) ** 2))
+    return {"psnr_db": round(float(psnr), 2), "reference_psnr_db": REF_PSNR_128SPP, "spp": spp,
+            "scene": "c1 BasicRayTracingWithC++ Cornell box 256x256", "vs": "4000spp.png (reference)",
+            "render_ms": round(dt * 1e3, 2)}
 
 
 def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, seconds):
