@@ -50,6 +50,7 @@ extern "C" {
 #define PT_FLAG_COUNT_FETCHES 0x4u /* count reference-algorithm fetches (implies NO_CULL, closest shadow) */
 #define PT_FLAG_WAVEFRONT 0x8u    /* staged wavefront pipeline instead of the persistent megakernel */
 #define PT_FLAG_REGEN 0x10u       /* path-regeneration state-machine kernel instead of the megakernel */
+#define PT_FLAG_NO_TILE_ORDER 0x20u /* megakernel: hand out tiles in fixed order, not longest-first */
 
 typedef struct pt_config {
   int width;          /* RenderPass::width  (OpenglRayTracing/main.cpp:83), e.g. 1920 */

@@ -71,6 +71,8 @@ struct RenderParams {
   int ovfDepth;
   unsigned long long* stats;  // [rays, nodes, tris, mats, texels]
   unsigned long long* rayShards;  // RAY_SHARDS ray counters (stride RAY_SHARD_STRIDE)
+  const int* tileOrder; // per-band tile order (null = identity), see reorderKernel
+  int* tileCost;        // per-tile cost of this frame (shader cycles), null = not recorded
 };
 
 struct TraceParams {
@@ -100,6 +102,9 @@ struct PackParams {
 };
 
 hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count);
+// tile order of the next frame: each queue band sorted by this frame's tile cost, descending
+constexpr int REORDER_MAX = 4096;  // largest band the one-block LDS sort handles
+hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, hipStream_t s);
 hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, int* nb);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull);
 hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb);

@@ -333,6 +333,53 @@ __global__ __launch_bounds__(BLOCK) void basicKernel(BasicParams p) {
   if ((threadIdx.x & 63) == 0 && rays) atomicAdd(reinterpret_cast<unsigned long long*>(p.stats), (unsigned long long)rays);
 }
 
+// ------------------------------------------------------------ tile order
+// One block per queue band: sort the band's tiles by the cost the megakernel
+// measured for them this frame (descending; ties by tile id), bitonic in LDS.
+// The next frame hands them out in that order (TileCursor), so the band's
+// long-path tiles start first. Progressive frames share camera and scene, so a
+// tile's cost is a good predictor of its cost in the next frame.
+__global__ __launch_bounds__(1024) void reorderKernel(const int* cost, int* order, int perQueue, int numItems) {
+  __shared__ unsigned long long key[REORDER_MAX];
+  const int q = blockIdx.x;
+  const int base = q * perQueue;
+  const int n = max(0, min(perQueue, numItems - base));
+  int size = 1;
+  while (size < n) size <<= 1;
+  for (int i = threadIdx.x; i < size; i += blockDim.x) {
+    unsigned long long k = 0;  // padding sorts last
+    if (i < n) {
+      const int t = base + i;
+      k = ((unsigned long long)(unsigned)max(cost[t], 1) << 32) | (unsigned)(0x7fffffff - t);
+    }
+    key[i] = k;
+  }
+  __syncthreads();
+  for (int k = 2; k <= size; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < size; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool desc = (i & k) == 0;  // descending overall
+          const unsigned long long a = key[i], b = key[l];
+          if (desc ? (a < b) : (a > b)) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) order[base + i] = 0x7fffffff - (int)(unsigned)(key[i] & 0xffffffffu);
+}
+
+hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, hipStream_t s) {
+  if (perQueue > REORDER_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(reorderKernel, dim3(NUM_QUEUES), dim3(1024), 0, s, cost, order, perQueue, numItems);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ render kernel
 __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
@@ -353,14 +400,16 @@ __global__ __launch_bounds__(BLOCK, PT_MIN_WAVES) void renderKernel(RenderParams
   const int sub = p.shardSize >> 3;        // wave tiles per shard-tile edge
   TileCursor cur;
   while (true) {
-    const int w = cur.next(p.queue, p.perQueue, p.numItems, home);
+    const int w = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder);
     if (w < 0) break;
+    const long long t0 = COUNT ? 0 : clock64();
     const int j = w / tilesPerShard, s = w - j * tilesPerShard;
     const int g = j * p.world + p.rank;  // global shard tile id (row-major)
     const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
     const int px = gx * p.shardSize + (s % sub) * 8 + (lane & 7);
     const int py = gy * p.shardSize + (s / sub) * 8 + (lane >> 3);
     if (px < p.width && py < p.height) shadePixel<INTEG, CULL, COUNT>(p, px, py, st, C);
+    if (!COUNT && p.tileCost && lane == 0) p.tileCost[w] = (int)min(clock64() - t0, (long long)0x7fffffff);
   }
   addRays(p.rayShards, C.rays);
   if (COUNT) {

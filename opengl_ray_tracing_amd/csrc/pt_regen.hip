@@ -242,7 +242,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
       const unsigned long long idle = __ballot(!active);
       if (idle == 0) break;
       if (cursor >= 64) {
-        const int item = cur.next(p.queue, p.perQueue, p.numItems, home);
+        const int item = cur.next(p.queue, p.perQueue, p.numItems, home, nullptr);
         if (item < 0) break;  // no tiles left for this wave
         tile = item;
         cursor = 0;

@@ -49,6 +49,9 @@ struct pt_ctx {
   // launch), cumulative fetch stats, padded sharded cumulative ray counters
   unsigned char* d_ctl = nullptr;
   int* d_ovf = nullptr;
+  int* d_cost = nullptr;   // per-tile cost of the last frame (megakernel)
+  int* d_order = nullptr;  // per-band tile order for the next frame
+  bool orderValid = false;
   size_t ovfInts = 0;
   // shards
   int shardSize = 32, shardsX = 0, shardsY = 0, numItems = 0, perQueue = 0;
@@ -171,7 +174,7 @@ void pt_destroy(pt_ctx* ctx) {
   if (ctx->own) (void)hipStreamSynchronize(ctx->own);
   dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
-  dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf);
+  dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
   freeWavefront(ctx);
   for (hipEvent_t e : ctx->evs) (void)hipEventDestroy(e);
@@ -565,9 +568,22 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   p.ovfDepth = ovfDepth;
   p.stats = stats;
   p.rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAYS);
+  // longest-tiles-first: each band's tiles in the order of the previous frame's cost
+  const bool ordered = !regen && !count && !(c.flags & PT_FLAG_NO_TILE_ORDER) && ctx->perQueue <= REORDER_MAX;
+  if (ordered && !ctx->d_cost) {
+    CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * sizeof(int)));
+    CK(hipMalloc(&ctx->d_order, (size_t)ctx->numItems * sizeof(int)));
+    ctx->orderValid = false;
+  }
+  p.tileOrder = ordered && ctx->orderValid ? ctx->d_order : nullptr;
+  p.tileCost = ordered ? ctx->d_cost : nullptr;
   CK(hipEventRecord(evb, ctx->stream));
   if (regen) CK(launchRegen(p, c.integrator, grid, ctx->stream, cull));
   else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
+  if (ordered) {
+    CK(launchReorder(ctx->d_cost, ctx->d_order, ctx->perQueue, ctx->numItems, ctx->stream));
+    ctx->orderValid = true;
+  }
   CK(hipEventRecord(eve, ctx->stream));
   ctx->launches++;
   return PT_OK;

@@ -205,16 +205,20 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
 // round-robin. One tile per atomic measured best:
 // claiming 2 or 4 per atomic, interleaving the queues or grouping an XCD's
 // queues into one band were all slower or neutral.
+// order (may be null = identity) permutes the tiles within each queue's band:
+// the megakernel hands out each band's most expensive tiles of the previous
+// frame first (renderKernel / reorderKernel), so long paths start early instead
+// of forming the frame's tail.
 struct TileCursor {
   int qi = 0;  // queues found empty (wave-uniform)
-  __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home) {
+  __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home, const int* order) {
     while (qi < NUM_QUEUES) {
       const int q = (home + qi) & (NUM_QUEUES - 1);
       int it = 0;
       if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
       it = __shfl(it, 0, 64);
       const int t = q * perQueue + it;
-      if (it < perQueue && t < numItems) return t;
+      if (it < perQueue && t < numItems) return order ? order[t] : t;
       qi++;
     }
     return -1;

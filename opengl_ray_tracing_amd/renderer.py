@@ -30,6 +30,7 @@ FLAG_CLOSEST_SHADOW = 0x2
 FLAG_COUNT_FETCHES = 0x4
 FLAG_WAVEFRONT = 0x8
 FLAG_REGEN = 0x10
+FLAG_NO_TILE_ORDER = 0x20
 
 
 @dataclass

@@ -127,3 +127,14 @@ def test_frame_kernels_agree(request, name, integrator):
         assert sb.rays >= sa.rays >= 0.95 * sb.rays
     else:
         assert sa.rays == sb.rays == sc.rays
+
+
+def test_tile_order_does_not_change_the_image(c4):
+    """Longest-tiles-first scheduling (default) only reorders work: frames after the first use the
+    previous frame's per-tile costs, and the image equals the fixed-order one bit for bit."""
+    from opengl_ray_tracing_amd import FLAG_NO_TILE_ORDER
+    cfg, tris, nodes, hdr = c4
+    a, sa = render_gpu(cfg, tris, nodes, hdr, frames=3)
+    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=3, flags=FLAG_NO_TILE_ORDER)
+    assert np.array_equal(a, b)
+    assert sa.rays == sb.rays
