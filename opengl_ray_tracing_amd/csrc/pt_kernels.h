@@ -10,6 +10,9 @@ constexpr int BLOCK = 256;        // 4 waves of 64
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 32
 #endif
+#ifndef PT_MIN_WAVES_LAMBERT
+#define PT_MIN_WAVES_LAMBERT 3    // Lambert megakernel: keep 3 waves/SIMD (<= 168 VGPRs, no spills)
+#endif
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif

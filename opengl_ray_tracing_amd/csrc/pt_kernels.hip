@@ -387,7 +387,7 @@ __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
 }
 
 template <int INTEG, bool CULL, bool COUNT>
-__global__ __launch_bounds__(BLOCK, PT_MIN_WAVES) void renderKernel(RenderParams p) {
+__global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_WAVES) void renderKernel(RenderParams p) {
   __shared__ int s_stack[LDS_STACK * BLOCK];
   Stack st;
   st.lds = s_stack + threadIdx.x;

@@ -242,11 +242,14 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
       const float* c = nodes + (size_t)R * 12;
       ra = make_float4(c[6], c[7], c[8], 0); rb = make_float4(c[9], c[10], c[11], 0);
     }
-    int lrr = lr, rrr = rr;
-    std::memcpy(&la.w, &lrr, 4);
-    std::memcpy(&lb.w, &rrr, 4);
-    bvh[4 * (size_t)k + 0] = la; bvh[4 * (size_t)k + 1] = lb;
-    bvh[4 * (size_t)k + 2] = ra; bvh[4 * (size_t)k + 3] = rb;
+    // children paired per component (left, right) so one packed op serves both boxes
+    float refs[2];
+    std::memcpy(&refs[0], &lr, 4);
+    std::memcpy(&refs[1], &rr, 4);
+    bvh[4 * (size_t)k + 0] = make_float4(la.x, ra.x, la.y, ra.y);
+    bvh[4 * (size_t)k + 1] = make_float4(la.z, ra.z, lb.x, rb.x);
+    bvh[4 * (size_t)k + 2] = make_float4(lb.y, rb.y, lb.z, rb.z);
+    bvh[4 * (size_t)k + 3] = make_float4(refs[0], refs[1], 0.0f, 0.0f);
   }
   int rootRef = encodeRef(1);
   if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);

@@ -53,6 +53,38 @@ __device__ __forceinline__ float hitAABB(V3 o, V3 inv, float4 lo, float4 hi, flo
   return (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
 }
 
+// Both children's hitAABB of one wide node. Node record (pt_runtime.cpp):
+// {L.lo.x, R.lo.x, L.lo.y, R.lo.y}, {L.lo.z, R.lo.z, L.hi.x, R.hi.x},
+// {L.hi.y, R.hi.y, L.hi.z, R.hi.z}, {left ref, right ref, -, -}: the slab
+// differences and products of the two boxes run as packed pairs
+// (v_pk_add_f32 / v_pk_mul_f32, the same IEEE operations as hitAABB); the
+// min/max reductions are hitAABB's, component by component.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+struct NodeHit {
+  float d1, d2;    // the reference's d for the left / right child
+  float t0l, t0r;  // slab entries (culling)
+  int lref, rref;
+};
+__device__ __forceinline__ void visitNode(const float4* nd, V3 o, V3 inv, NodeHit& h) {
+  const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+  const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+  const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+  const f32x2 lox = {q0.x, q0.y}, loy = {q0.z, q0.w}, loz = {q1.x, q1.y};
+  const f32x2 hix = {q1.z, q1.w}, hiy = {q2.x, q2.y}, hiz = {q2.z, q2.w};
+  const f32x2 fx = (hix - ox) * ix, fy = (hiy - oy) * iy, fz = (hiz - oz) * iz;
+  const f32x2 nx = (lox - ox) * ix, ny = (loy - oy) * iy, nz = (loz - oz) * iz;
+  float t1 = fminf(fmaxf(fx.x, nx.x), fminf(fmaxf(fy.x, ny.x), fmaxf(fz.x, nz.x)));
+  float t0 = fmaxf(fminf(fx.x, nx.x), fmaxf(fminf(fy.x, ny.x), fminf(fz.x, nz.x)));
+  h.t0l = t0;
+  h.d1 = (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
+  t1 = fminf(fmaxf(fx.y, nx.y), fminf(fmaxf(fy.y, ny.y), fmaxf(fz.y, nz.y)));
+  t0 = fmaxf(fminf(fx.y, nx.y), fmaxf(fminf(fy.y, ny.y), fminf(fz.y, nz.y)));
+  h.t0r = t0;
+  h.d2 = (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
+  h.lref = __float_as_int(q3.x);
+  h.rref = __float_as_int(q3.y);
+}
+
 // hitTriangle IS:251-301, accept/reject and distance only. With the stored unit
 // normal Ng = normalize(cross(p2-p1,p3-p1)) and w = dot(Ng,p1) (computed on the
 // host in the reference's order) this rounds exactly like the reference: the
@@ -111,12 +143,10 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
   while (true) {
     // node phase
     while (ref >= 0) {
-      const float4* nd = S.bvh + 4 * (size_t)ref;
-      float4 la = nd[0], lb = nd[1], ra = nd[2], rb = nd[3];
-      int lref = __float_as_int(la.w), rref = __float_as_int(lb.w);
-      float t0l, t0r;
-      float d1 = hitAABB(o, inv, la, lb, t0l);
-      float d2 = hitAABB(o, inv, ra, rb, t0r);
+      NodeHit nh;
+      visitNode(S.bvh + 4 * (size_t)ref, o, inv, nh);
+      const int lref = nh.lref, rref = nh.rref;
+      const float d1 = nh.d1, d2 = nh.d2, t0l = nh.t0l, t0r = nh.t0r;
       bool h1 = (lref != REF_NONE) && d1 > 0.0f;
       bool h2 = (rref != REF_NONE) && d2 > 0.0f;
       if (COUNT) C.nodes += 1u + (lref != REF_NONE) + (rref != REF_NONE);

@@ -169,12 +169,10 @@ __global__ __launch_bounds__(BLOCK) void wfTraceKernel(WFTraceParams p) {
       }
       leafI++;
     } else {
-      const float4* nd = S.bvh + 4 * (size_t)ref;
-      float4 la = nd[0], lb = nd[1], ra = nd[2], rb = nd[3];
-      int lref = __float_as_int(la.w), rref = __float_as_int(lb.w);
-      float t0l, t0r;
-      float d1 = hitAABB(o, inv, la, lb, t0l);
-      float d2 = hitAABB(o, inv, ra, rb, t0r);
+      NodeHit nh;
+      visitNode(S.bvh + 4 * (size_t)ref, o, inv, nh);
+      const int lref = nh.lref, rref = nh.rref;
+      const float d1 = nh.d1, d2 = nh.d2, t0l = nh.t0l, t0r = nh.t0r;
       bool h1 = (lref != REF_NONE) && d1 > 0.0f;
       bool h2 = (rref != REF_NONE) && d2 > 0.0f;
       if (CULL) {
