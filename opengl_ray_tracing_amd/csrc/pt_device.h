@@ -174,7 +174,10 @@ __device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
   y = 1.0f - y;
   float phi = 2.0f * PT_PI * (x - 0.5f);
   float theta = PT_PI * (y - 0.5f);
-  return v3(ptm_cosf(theta) * ptm_cosf(phi), ptm_sinf(theta), ptm_cosf(theta) * ptm_sinf(phi));
+  float st, ct, sp, cp;
+  ptm_sincosf(theta, &st, &ct);
+  ptm_sincosf(phi, &sp, &cp);
+  return v3(ct * cp, st, ct * sp);
 }
 // hdrPdf IS:655-666 (sin of the elevation: reference quirk kept)
 __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
@@ -185,6 +188,25 @@ __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
   float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
   float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
   return pdf * p_convert;
+}
+
+// hdrColor(L) and hdrPdf(L) of the same direction (every MIS use pairs them):
+// one toSphericalCoord, the same operations and results as the two calls.
+__device__ __forceinline__ void hdrColorPdf(const Env& e, V3 L, V3& color, float& pdf) {
+  if (!e.hdr) {
+    color = v3(0, 0, 0);
+  }
+  float u, w;
+  toSpherical(normalize(L), u, w);
+  if (e.hdr) {
+    float4 c = texNearest(e.hdr, e.w, e.h, u, w);
+    color = v3(c.x, c.y, c.z);
+  }
+  const float p = e.cache ? texNearest(e.cache, e.w, e.h, u, w).z : 0.0f;
+  const float theta = PT_PI * (0.5f - w);
+  const float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
+  const float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
+  pdf = p * p_convert;
 }
 
 // ------------------------------------------------------------ BRDF IS:386-711
@@ -345,22 +367,26 @@ __device__ __forceinline__ V3 sampleHemisphereRand(uint32_t& seed) {
   float z = randf(seed);
   float r = fmaxf(0.0f, sqrtf(1.0f - z * z));
   float phi = 2.0f * PT_PI * randf(seed);
-  return v3(r * ptm_cosf(phi), r * ptm_sinf(phi), z);
+  float s, c;
+  ptm_sincosf(phi, &s, &c);  // the same bits as ptm_sinf / ptm_cosf, one range reduction
+  return v3(r * c, r * s, z);
 }
 // SampleCosineHemisphere IS:485-496
 __device__ __forceinline__ V3 sampleCosine(float xi_1, float xi_2, V3 N) {
   float r = sqrtf(xi_1);
   float theta = xi_2 * 2.0f * PT_PI;
-  float x = r * ptm_cosf(theta);
-  float y = r * ptm_sinf(theta);
+  float st, ct;
+  ptm_sincosf(theta, &st, &ct);
+  float x = r * ct;
+  float y = r * st;
   float z = sqrtf(1.0f - x * x - y * y);
   return toNormalHemisphere(v3(x, y, z), N);
 }
 // SampleGTR2 IS:499-516 / SampleGTR1 IS:519-536
 __device__ __forceinline__ V3 sampleGTR(float xi_1, float xi_2, V3 V, V3 N, float alpha, bool gtr1) {
   float phi_h = 2.0f * PT_PI * xi_1;
-  float sin_phi_h = ptm_sinf(phi_h);
-  float cos_phi_h = ptm_cosf(phi_h);
+  float sin_phi_h, cos_phi_h;
+  ptm_sincosf(phi_h, &sin_phi_h, &cos_phi_h);
   float cos_theta_h;
   if (gtr1)
     cos_theta_h = sqrtf((1.0f - ptm_powf(alpha * alpha, 1.0f - xi_2)) / (1.0f - alpha * alpha));

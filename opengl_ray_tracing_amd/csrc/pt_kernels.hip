@@ -119,8 +119,9 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
     if (dot(N, Ldir) > 0.0f) {
       if (!tr.occluded(hit.P, Ldir)) {
         V3 L = Ldir;
-        V3 color = hdrColor(env, L);
-        float pdf_light = hdrPdf(env, L);
+        V3 color;
+        float pdf_light;
+        hdrColorPdf(env, L, color, pdf_light);
         if (count) C.texels += 2;
         V3 f_r = brdfIso(V, N, L, hit.m);
         float pdf_brdf = brdfPdf(V, N, L, hit.m);
@@ -142,8 +143,9 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
     float pdf_brdf = brdfPdf(V, N, L, hit.m);
     if (pdf_brdf <= 0.0f) break;
     if (!isHit) {
-      V3 color = hdrColor(env, L);
-      float pdf_light = hdrPdf(env, L);
+      V3 color;
+      float pdf_light;
+      hdrColorPdf(env, L, color, pdf_light);
       if (count) C.texels += 2;
       float mis_weight = misWeight(pdf_brdf, pdf_light);
       V3 c = ((history * mis_weight) * color) * f_r;

@@ -115,8 +115,9 @@ __device__ __forceinline__ bool continueFromHit(const RenderParams& p, PathState
   bool shadow = false;
   if (dot(N, Ldir) > 0.0f) {  // IS:775-790; added if the shadow ray escapes
     V3 L = Ldir;
-    V3 color = hdrColor(p.env, L);
-    float pdf_light = hdrPdf(p.env, L);
+    V3 color;
+    float pdf_light;
+    hdrColorPdf(p.env, L, color, pdf_light);
     V3 f_r = brdfIso(V, N, L, hit.m);
     float pdf_brdf = brdfPdf(V, N, L, hit.m);
     float mis_weight = misWeight(pdf_light, pdf_brdf);
@@ -187,8 +188,9 @@ __device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int
   // K_BOUNCE
   if (INTEG == 2) {
     if (tri < 0) {  // IS:819-829
-      V3 c = hdrColor(p.env, s.d);
-      float pdf_light = hdrPdf(p.env, s.d);
+      V3 c;
+      float pdf_light;
+      hdrColorPdf(p.env, s.d, c, pdf_light);
       float mis_weight = misWeight(s.pdfB, pdf_light);
       V3 cc = ((s.hist * mis_weight) * c) * s.f_r;
       s.Lo = s.Lo + (cc * s.cosL) / s.pdfB;

@@ -250,8 +250,9 @@ __device__ __forceinline__ uint32_t prepareMIS(const WFParams& p, int pid, int p
   if (dot(N, Ldir) > 0.0f) {
     // the unoccluded contribution (IS:781-789), added by the next stage if the ray escapes
     V3 L = Ldir;
-    V3 color = hdrColor(p.env, L);
-    float pdf_light = hdrPdf(p.env, L);
+    V3 color;
+    float pdf_light;
+    hdrColorPdf(p.env, L, color, pdf_light);
     V3 f_r = brdfIso(V, N, L, hit.m);
     float pdf_brdf = brdfPdf(V, N, L, hit.m);
     float mis_weight = misWeight(pdf_light, pdf_brdf);
@@ -339,8 +340,9 @@ __global__ __launch_bounds__(BLOCK) void wfShadeKernel(WFParams p, int stage) {
             int2 h = S.hit[pid];
             V3 o = xyz(S.rayO[pid]), L = xyz(S.rayD[pid]);
             if (h.x < 0) {  // IS:819-829
-              V3 c = hdrColor(p.env, L);
-              float pdf_light = hdrPdf(p.env, L);
+              V3 c;
+              float pdf_light;
+              hdrColorPdf(p.env, L, c, pdf_light);
               float mis_weight = misWeight(pdf_brdf, pdf_light);
               V3 cc = ((history * mis_weight) * c) * f_r;
               Lo = Lo + (cc * NdotL) / pdf_brdf;
