@@ -106,6 +106,11 @@ int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
 /* PT_BASIC_CPU_COMPAT shape list: n x 24 f32 records (layout in pt_scene.h). */
 int pt_upload_shapes(pt_ctx* ctx, const float* shapes, int n);
 
+/* calculateHdrCache (ImportanceSampling_LowDiscrepancySequence/main.cpp:555-652)
+ * computed on this context's GPU; output as pt_hdr_cache (w*h*3 f32: sample x,
+ * sample y, pdf), bit-identical to it. pt_upload_env with cache = NULL uses it. */
+int pt_hdr_cache_device(pt_ctx* ctx, const float* hdr, int w, int h, float* cache_out);
+
 /* One display() (OpenglRayTracing/main.cpp:558-603): 1 spp per owned pixel and
  * the running-mean update of the device-resident accumulation (pass1.fsh:868-871);
  * frameCounter = 0 resets the mean (mix weight 1). eye[3]; cameraRotate[16]

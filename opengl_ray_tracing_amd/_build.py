@@ -42,6 +42,7 @@ SOURCES = {
                                                            INCLUDE / "pt_fmath.h"]),
     "pt_regen.o": ("hip", CSRC / "pt_regen.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h", CSRC / "pt_trace.h",
                                                    INCLUDE / "pt_fmath.h"]),
+    "pt_envcache.o": ("hip", CSRC / "pt_envcache.hip", [CSRC / "pt_kernels.h"]),
     "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", CSRC / "pt_wavefront.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
                                                        INCLUDE / "pt_fmath.h"]),
     "scene.o": ("cxx", CSRC / "scene.cpp", [INCLUDE / "pt_scene.h"]),

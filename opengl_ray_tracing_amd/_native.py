@@ -90,6 +90,7 @@ SIGNATURES = {
     "pt_hdr_decode": (C.c_int, [C.c_void_p, C.c_int64, c_int_p, c_int_p, C.POINTER(c_float_p)]),
     "pt_free": (None, [C.c_void_p]),
     "pt_hdr_cache": (C.c_int, [c_float_p, C.c_int, C.c_int, c_float_p]),
+    "pt_hdr_cache_device": (C.c_int, [C.c_void_p, c_float_p, C.c_int, C.c_int, c_float_p]),
     "pt_image_write_pfm": (C.c_int, [C.c_char_p, c_float_p, C.c_int, C.c_int, C.c_int]),
     "pt_image_write_png": (C.c_int, [C.c_char_p, c_float_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_int]),
 }

@@ -1,0 +1,116 @@
+// pt_envcache.hip -- calculateHdrCache (ImportanceSampling_LowDiscrepancySequence/
+// main.cpp:555-652) on the GPU, bit-identical to the host restatement
+// (scene.cpp pt_hdr_cache): every floating-point sum runs in the reference's
+// order. Its one inherently sequential step, the float sum of all luminances
+// in scanline order, is a single dependent chain; one wave streams the values
+// through LDS and lane 0 adds them. The per-column sums and prefix sums are
+// one thread per column (serial over rows, as the reference), the row prefix
+// is one thread, and the sample table is one thread per texel (two
+// lower_bound searches).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_kernels.h"
+
+namespace pt {
+
+// lum = 0.2 * R + 0.7 * G + 0.1 * B in double (the reference's double literals), stored as float
+__global__ void hdrLumKernel(const float* hdr, float* lum, int n) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double R = hdr[3 * (size_t)k], G = hdr[3 * (size_t)k + 1], B = hdr[3 * (size_t)k + 2];
+  lum[k] = (float)((0.2 * R + 0.7 * G) + 0.1 * B);
+}
+
+// lumSum += lum, k = 0 .. n-1 in order (main.cpp:561-570)
+__global__ __launch_bounds__(64) void hdrSumKernel(const float* lum, int n, float* out) {
+  __shared__ float buf[4096];
+  float sum = 0.0f;
+  for (int base = 0; base < n; base += 4096) {
+    const int m = min(4096, n - base);
+    for (int i = threadIdx.x; i < m; i += 64) buf[i] = lum[base + i];
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 0; i < m; i++) sum += buf[i];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sum;
+}
+
+// pdf = lum / lumSum (main.cpp:573-575)
+__global__ void hdrPdfKernel(float* pdf, int n, const float* lumSum) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  pdf[k] /= *lumSum;
+}
+
+// per column j: margin[j] = sum_i pdf[i][j] (rows in order), then the
+// conditional CDF over rows, stored column-major cdfY[j * h + i] (main.cpp:578-605)
+__global__ void hdrColumnKernel(const float* pdf, int w, int h, float* margin, float* cdfY) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= w) return;
+  float m = 0.0f;
+  for (int i = 0; i < h; i++) m += pdf[(size_t)i * w + j];
+  margin[j] = m;
+  float* col = cdfY + (size_t)j * h;
+  float acc = 0.0f;
+  for (int i = 0; i < h; i++) {
+    const float v = pdf[(size_t)i * w + j] / m;
+    acc = i == 0 ? v : acc + v;
+    col[i] = acc;
+  }
+}
+
+// cdfX = prefix sum of margin (main.cpp:584-586)
+__global__ void hdrRowPrefixKernel(const float* margin, int w, float* cdfX) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  float acc = 0.0f;
+  for (int j = 0; j < w; j++) {
+    acc = j == 0 ? margin[0] : acc + margin[j];
+    cdfX[j] = acc;
+  }
+}
+
+__device__ __forceinline__ int lowerBound(const float* a, int n, float v) {
+  int lo = 0, hi = n;  // first index with !(a[idx] < v)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// sample table (main.cpp:617-640): (x/w, y/h, pdf) per texel; the row CDF index
+// is clamped like the host restatement (the reference reads past the end there)
+__global__ void hdrSampleKernel(const float* pdf, const float* cdfX, const float* cdfY, int w, int h, float4* cache) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= w * h) return;
+  const int i = k / w, j = k - i * w;
+  const float xi_1 = (float)i / (float)h;
+  const float xi_2 = (float)j / (float)w;
+  const int x = lowerBound(cdfX, w, xi_1);
+  const int xr = x < w ? x : w - 1;
+  const int y = lowerBound(cdfY + (size_t)xr * h, h, xi_2);
+  cache[k] = make_float4((float)x / (float)w, (float)y / (float)h, pdf[k], 0.0f);
+}
+
+// scratch: 2*w*h + 2*w + 1 floats
+hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s) {
+  const int n = w * h;
+  float* pdf = scratch;
+  float* cdfY = pdf + n;
+  float* margin = cdfY + n;
+  float* cdfX = margin + w;
+  float* lumSum = cdfX + w;
+  const int B = 256;
+  hipLaunchKernelGGL(hdrLumKernel, dim3((n + B - 1) / B), dim3(B), 0, s, hdr, pdf, n);
+  hipLaunchKernelGGL(hdrSumKernel, dim3(1), dim3(64), 0, s, pdf, n, lumSum);
+  hipLaunchKernelGGL(hdrPdfKernel, dim3((n + B - 1) / B), dim3(B), 0, s, pdf, n, lumSum);
+  hipLaunchKernelGGL(hdrColumnKernel, dim3((w + 63) / 64), dim3(64), 0, s, pdf, w, h, margin, cdfY);
+  hipLaunchKernelGGL(hdrRowPrefixKernel, dim3(1), dim3(1), 0, s, margin, w, cdfX);
+  hipLaunchKernelGGL(hdrSampleKernel, dim3((n + B - 1) / B), dim3(B), 0, s, pdf, cdfX, cdfY, w, h, cache);
+  return hipGetLastError();
+}
+
+}  // namespace pt

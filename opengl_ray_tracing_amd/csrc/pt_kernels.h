@@ -104,6 +104,8 @@ struct PackParams {
   long count;
 };
 
+// calculateHdrCache on the device (pt_envcache.hip); scratch: 2*w*h + 2*w + 1 floats
+hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);
 hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count);
 // tile order of the next frame: each queue band sorted by this frame's tile cost, descending
 constexpr int REORDER_MAX = 4096;  // largest band the one-block LDS sort handles

@@ -284,6 +284,25 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
   return PT_OK;
 }
 
+// calculateHdrCache of host image hdr (w*h*3) into the device table out (w*h float4)
+static int deviceHdrCache(pt_ctx* ctx, const float* hdr, int w, int h, float4* out) {
+  const size_t n = (size_t)w * h;
+  float* d3 = nullptr;
+  float* scratch = nullptr;
+  CK(hipMalloc(&d3, n * 3 * sizeof(float)));
+  if (hipMalloc(&scratch, (2 * n + 2 * (size_t)w + 1) * sizeof(float)) != hipSuccess) {
+    hipFree(d3);
+    return fail(ctx, PT_E_NOMEM, "hdr cache scratch");
+  }
+  hipError_t e = hipMemcpyAsync(d3, hdr, n * 3 * sizeof(float), hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = launchHdrCache(d3, w, h, out, scratch, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  hipFree(d3);
+  hipFree(scratch);
+  if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("hdr cache: ") + hipGetErrorString(e));
+  return PT_OK;
+}
+
 int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache) {
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
@@ -293,23 +312,40 @@ int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
   if (!hdr) return PT_OK;
   if (w <= 0 || h <= 0) return PT_E_INVALID;
   const size_t n = (size_t)w * h;
-  std::vector<float> own;
-  if (!cache) {
-    own.resize(n * 3);
-    if (pt_hdr_cache(hdr, w, h, own.data()) != 0) return fail(ctx, PT_E_INVALID, "hdr cache failed");
-    cache = own.data();
-  }
-  std::vector<float4> a(n), b(n);
-  for (size_t k = 0; k < n; k++) {
-    a[k] = make_float4(hdr[3 * k], hdr[3 * k + 1], hdr[3 * k + 2], 0.0f);
-    b[k] = make_float4(cache[3 * k], cache[3 * k + 1], cache[3 * k + 2], 0.0f);
-  }
+  std::vector<float4> a(n);
+  for (size_t k = 0; k < n; k++) a[k] = make_float4(hdr[3 * k], hdr[3 * k + 1], hdr[3 * k + 2], 0.0f);
   CK(hipMalloc(&ctx->d_hdr, n * sizeof(float4)));
   CK(hipMalloc(&ctx->d_cache, n * sizeof(float4)));
   CK(hipMemcpy(ctx->d_hdr, a.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-  CK(hipMemcpy(ctx->d_cache, b.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  if (cache) {
+    for (size_t k = 0; k < n; k++) a[k] = make_float4(cache[3 * k], cache[3 * k + 1], cache[3 * k + 2], 0.0f);
+    CK(hipMemcpy(ctx->d_cache, a.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  } else {
+    int rc = deviceHdrCache(ctx, hdr, w, h, ctx->d_cache);  // calculateHdrCache on the GPU
+    if (rc) return rc;
+  }
   ctx->hdrW = w;
   ctx->hdrH = h;
+  return PT_OK;
+}
+
+int pt_hdr_cache_device(pt_ctx* ctx, const float* hdr, int w, int h, float* cache_out) {
+  if (!ctx || !hdr || !cache_out || w <= 0 || h <= 0) return PT_E_INVALID;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  const size_t n = (size_t)w * h;
+  float4* d = nullptr;
+  CK(hipMalloc(&d, n * sizeof(float4)));
+  int rc = deviceHdrCache(ctx, hdr, w, h, d);
+  std::vector<float4> b(rc ? 0 : n);
+  if (!rc && hipMemcpy(b.data(), d, n * sizeof(float4), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(ctx, PT_E_HIP, "pt_hdr_cache_device: copy");
+  hipFree(d);
+  if (rc) return rc;
+  for (size_t k = 0; k < n; k++) {
+    cache_out[3 * k] = b[k].x;
+    cache_out[3 * k + 1] = b[k].y;
+    cache_out[3 * k + 2] = b[k].z;
+  }
   return PT_OK;
 }
 

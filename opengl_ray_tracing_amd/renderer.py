@@ -100,6 +100,14 @@ class Renderer:
         n = np.ascontiguousarray(nodes, np.float32).reshape(-1, 12)
         self._ck(self._lib.pt_upload_scene(self._h, _fp(t), t.shape[0], _fp(n), n.shape[0]), "pt_upload_scene")
 
+    def hdr_cache_device(self, hdr: np.ndarray) -> np.ndarray:
+        """calculateHdrCache on this context's GPU, (h, w, 3) like scene.calculate_hdr_cache."""
+        h = np.ascontiguousarray(hdr, np.float32)
+        hh, ww = h.shape[:2]
+        out = np.empty((hh, ww, 3), np.float32)
+        self._ck(self._lib.pt_hdr_cache_device(self._h, _fp(h), ww, hh, _fp(out)), "pt_hdr_cache_device")
+        return out
+
     def upload_env(self, hdr, cache=None):
         if hdr is None:
             self._ck(self._lib.pt_upload_env(self._h, None, 0, 0, None), "pt_upload_env")

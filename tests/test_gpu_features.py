@@ -231,3 +231,16 @@ def test_sample_parallel_streams():
     for f in range(frames):
         acc, _ = o.render(w, h, "lambert", f, eye, rot, accum=acc, sample_rank=1, sample_world=world)
     assert np.array_equal(parts[1], acc)
+
+
+@pytest.mark.parametrize("name", ["peppermint_powerplant_4k.hdr", "san_giuseppe_bridge_blurred.hdr"])
+def test_hdr_cache_on_gpu_equals_host(name):
+    """calculateHdrCache on the GPU (pt_envcache.hip) == the host restatement, bit for bit."""
+    from pathlib import Path
+
+    from opengl_ray_tracing_amd import calculate_hdr_cache, load_hdr
+    hdr = load_hdr(Path(__file__).parent / "golden" / name)
+    host = calculate_hdr_cache(hdr)
+    with Renderer(8, 8) as r:
+        dev = r.hdr_cache_device(hdr)
+    assert np.array_equal(dev.view(np.uint32), host.view(np.uint32))
