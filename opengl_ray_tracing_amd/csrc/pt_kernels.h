@@ -107,9 +107,11 @@ struct PackParams {
 // calculateHdrCache on the device (pt_envcache.hip); scratch: 2*w*h + 2*w + 1 floats
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);
 hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count);
-// tile order of the next frame: each queue band sorted by this frame's tile cost, descending
-constexpr int REORDER_MAX = 4096;  // largest band the one-block LDS sort handles
-hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, hipStream_t s);
+// tile order of the next frame: each queue band's groups of `group` consecutive
+// tiles sorted by this frame's summed cost, descending (tiles inside a group keep
+// their order, which keeps neighbouring tiles together for the caches)
+constexpr int REORDER_MAX = 4096;  // most groups per band the one-block LDS sort handles
+hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, int group, hipStream_t s);
 hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, int* nb);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull);
 hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb);

@@ -341,20 +341,26 @@ __global__ __launch_bounds__(BLOCK) void basicKernel(BasicParams p) {
 // The next frame hands them out in that order (TileCursor), so the band's
 // long-path tiles start first. Progressive frames share camera and scene, so a
 // tile's cost is a good predictor of its cost in the next frame.
-__global__ __launch_bounds__(1024) void reorderKernel(const int* cost, int* order, int perQueue, int numItems) {
+__global__ __launch_bounds__(1024) void reorderKernel(const int* cost, int* order, int perQueue, int numItems,
+                                                       int group) {
   __shared__ unsigned long long key[REORDER_MAX];
+  __shared__ int partialPos;
   const int q = blockIdx.x;
   const int base = q * perQueue;
   const int n = max(0, min(perQueue, numItems - base));
+  const int ng = (n + group - 1) / group;  // groups of `group` consecutive tiles (the last may be short)
+  const int lastSize = n - (ng - 1) * group;
   int size = 1;
-  while (size < n) size <<= 1;
-  for (int i = threadIdx.x; i < size; i += blockDim.x) {
+  while (size < ng) size <<= 1;
+  for (int g = threadIdx.x; g < size; g += blockDim.x) {
     unsigned long long k = 0;  // padding sorts last
-    if (i < n) {
-      const int t = base + i;
-      k = ((unsigned long long)(unsigned)max(cost[t], 1) << 32) | (unsigned)(0x7fffffff - t);
+    if (g < ng) {
+      unsigned long long c = 0;
+      const int t0 = base + g * group, t1 = min(t0 + group, base + n);
+      for (int t = t0; t < t1; t++) c += (unsigned)max(cost[t], 1);
+      k = (min(c, 0xffffffffull) << 32) | (unsigned)(0x7fffffff - g);
     }
-    key[i] = k;
+    key[g] = k;
   }
   __syncthreads();
   for (int k = 2; k <= size; k <<= 1) {
@@ -373,12 +379,20 @@ __global__ __launch_bounds__(1024) void reorderKernel(const int* cost, int* orde
       __syncthreads();
     }
   }
-  for (int i = threadIdx.x; i < n; i += blockDim.x) order[base + i] = 0x7fffffff - (int)(unsigned)(key[i] & 0xffffffffu);
+  for (int r = threadIdx.x; r < ng; r += blockDim.x)
+    if (0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu) == ng - 1) partialPos = r;
+  __syncthreads();
+  for (int r = threadIdx.x; r < ng; r += blockDim.x) {
+    const int g = 0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu);
+    const int off = r * group - (r > partialPos ? group - lastSize : 0);
+    const int len = g == ng - 1 ? lastSize : group;
+    for (int k = 0; k < len; k++) order[base + off + k] = base + g * group + k;
+  }
 }
 
-hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, hipStream_t s) {
-  if (perQueue > REORDER_MAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(reorderKernel, dim3(NUM_QUEUES), dim3(1024), 0, s, cost, order, perQueue, numItems);
+hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, int group, hipStream_t s) {
+  if ((perQueue + group - 1) / group > REORDER_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(reorderKernel, dim3(NUM_QUEUES), dim3(1024), 0, s, cost, order, perQueue, numItems, group);
   return hipGetLastError();
 }
 

@@ -22,6 +22,10 @@
 
 using namespace pt;
 
+#ifndef PT_TILE_GROUP
+#define PT_TILE_GROUP 1  // tiles ordered by cost in groups of this many consecutive tiles (1 measured best)
+#endif
+
 
 struct pt_ctx {
   pt_config cfg{};
@@ -608,7 +612,9 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   p.stats = stats;
   p.rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAYS);
   // longest-tiles-first: each band's tiles in the order of the previous frame's cost
-  const bool ordered = !regen && !count && !(c.flags & PT_FLAG_NO_TILE_ORDER) && ctx->perQueue <= REORDER_MAX;
+  const int group = std::max(1, PT_TILE_GROUP);
+  const bool ordered = !regen && !count && !(c.flags & PT_FLAG_NO_TILE_ORDER) &&
+                       (ctx->perQueue + group - 1) / group <= REORDER_MAX;
   if (ordered && !ctx->d_cost) {
     CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * sizeof(int)));
     CK(hipMalloc(&ctx->d_order, (size_t)ctx->numItems * sizeof(int)));
@@ -620,7 +626,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   if (regen) CK(launchRegen(p, c.integrator, grid, ctx->stream, cull));
   else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
   if (ordered) {
-    CK(launchReorder(ctx->d_cost, ctx->d_order, ctx->perQueue, ctx->numItems, ctx->stream));
+    CK(launchReorder(ctx->d_cost, ctx->d_order, ctx->perQueue, ctx->numItems, group, ctx->stream));
     ctx->orderValid = true;
   }
   CK(hipEventRecord(eve, ctx->stream));
