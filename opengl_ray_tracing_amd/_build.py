@@ -29,6 +29,11 @@ HIP_FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
     # exact single-rounding float semantics, matching the CPU checker
     "-ffp-contract=off",
+    # no SLP packing of the scalar shading/triangle code into v_pk_* pairs: the
+    # lane shuffles it needs raised the MIS megakernel to 239 VGPRs (129 -> 167
+    # Lambert / 187 MIS without it) and cost 4-6 % per frame on c2/c3/c4
+    # (tools/tune.py); visitNode's explicit float2 slab pairs stay packed
+    "-fno-slp-vectorize",
     "-Wall", "-Wno-unused-function",
 ]
 CXX_FLAGS = ["-O2", "-fPIC", "-pthread", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall",
@@ -94,9 +99,10 @@ def variant_lib(name: str) -> Path:
     return VARIANTS / f"libpt_{name}.so"
 
 
-def build_variant(name: str, defines: dict) -> Path:
-    """A tuning build of libpt.so with extra -D defines (e.g. PT_MIN_WAVES, PT_LDS_STACK),
-    kept in-tree under _variants/ so tools/tune.py can A/B it on the GPU box."""
+def build_variant(name: str, defines: dict, hip_flags=()) -> Path:
+    """A tuning build of libpt.so with extra -D defines (e.g. PT_MIN_WAVES, PT_LDS_STACK)
+    and extra hipcc flags, kept in-tree under _variants/ so tools/tune.py can A/B it on
+    the GPU box."""
     out_dir = VARIANTS / name
     out_dir.mkdir(parents=True, exist_ok=True)
     dflags = [f"-D{k}={v}" for k, v in defines.items()]
@@ -106,7 +112,7 @@ def build_variant(name: str, defines: dict) -> Path:
         out = out_dir / obj
         objs.append(out)
         if kind == "hip":
-            _run([HIPCC, *HIP_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
+            _run([HIPCC, *HIP_FLAGS, *hip_flags, *dflags, *inc, "-c", str(src), "-o", str(out)])
         else:
             _run(["g++", *CXX_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
     lib = variant_lib(name)

@@ -92,10 +92,14 @@ __device__ __forceinline__ float sobolf(uint32_t d, uint32_t i) {
 __device__ __forceinline__ uint32_t grayCode(uint32_t i) { return i ^ (i >> 1); }
 
 // CranleyPattersonRotation IS:118-136
-__device__ __forceinline__ void cranleyPatterson(int px, int py, float& u_, float& v_) {
+// split into the per-pixel shift (constant across bounces and frames) and its
+// application, so a path computes the shift once
+__device__ __forceinline__ void cranleyPattersonShift(int px, int py, float& u, float& v) {
   uint32_t pseed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + 59u * 26699u) | 1u;
-  float u = (float)wang(pseed) / 4294967296.0f;
-  float v = (float)wang(pseed) / 4294967296.0f;
+  u = (float)wang(pseed) / 4294967296.0f;
+  v = (float)wang(pseed) / 4294967296.0f;
+}
+__device__ __forceinline__ void cranleyPattersonApply(float u, float v, float& u_, float& v_) {
   float x = u_ + u;
   if (x > 1.0f) x -= 1.0f;
   if (x < 0.0f) x += 1.0f;
@@ -104,6 +108,11 @@ __device__ __forceinline__ void cranleyPatterson(int px, int py, float& u_, floa
   if (y < 0.0f) y += 1.0f;
   u_ = x;
   v_ = y;
+}
+__device__ __forceinline__ void cranleyPatterson(int px, int py, float& u_, float& v_) {
+  float u, v;
+  cranleyPattersonShift(px, py, u, v);
+  cranleyPattersonApply(u, v, u_, v_);
 }
 
 // ------------------------------------------------------------ material

@@ -16,7 +16,12 @@ constexpr int BLOCK = 256;        // 4 waves of 64
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
-constexpr int LDS_STACK = PT_LDS_STACK;  // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
+constexpr int LDS_STACK = PT_LDS_STACK;
+#ifndef PT_LDS_NODES
+#define PT_LDS_NODES 256
+#endif
+// top-of-tree nodes (breadth-first from the root) the megakernel keeps in LDS, 64 B each
+constexpr int LDS_NODES = PT_LDS_NODES;  // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
 #ifndef PT_NUM_QUEUES
 #define PT_NUM_QUEUES 32
 #endif
@@ -41,7 +46,8 @@ constexpr int MAX_TRIS = (1 << (31 - LEAF_CNT_BITS)) - 1;
 struct SceneView {
   const float4* geo;   // 4 float4 per triangle: (p1, w=dot(Ng,p1)), (p2, 0), (p3, 0), (Ng, 0)
   const float* attr;   // 36 f32 per triangle: the Triangle_encoded record (normals, material)
-  const float4* bvh;   // 4 float4 per reference node id: (L.AA, Lref) (L.BB, Rref) (R.AA, -) (R.BB, -)
+  const float4* bvh;   // 4 float4 per device node id (pt_runtime.cpp: top of the tree first, breadth-first)
+  int nTop;            // device ids [0, nTop) are the top of the tree, staged in LDS by the megakernel
   int rootRef;         // encoded reference to node 1
   int nTri;
 };

@@ -34,9 +34,10 @@ struct Tracer {
   const SceneView& S;
   Stack& st;
   Counters& C;
+  const float4* top;  // LDS copy of the top of the tree (null = none)
   __device__ __forceinline__ bool closest(V3 o, V3 d, Hit& h) {
     float t;
-    int tri = traceRay<false, CULL, COUNT>(S, o, d, t, st, C);
+    int tri = traceRay<false, CULL, COUNT, Stack, (LDS_NODES > 0)>(S, o, d, t, st, C, false, top);
     if (tri < 0) return false;
     finishHit(S, tri, o, d, t, h);
     return true;
@@ -44,7 +45,7 @@ struct Tracer {
   __device__ __forceinline__ bool occluded(V3 o, V3 d) {
     float t;
     // COUNT reproduces the reference's closest-hit shadow query fetch by fetch
-    return traceRay<!COUNT, CULL, COUNT>(S, o, d, t, st, C) >= 0;
+    return traceRay<!COUNT, CULL, COUNT, Stack, (LDS_NODES > 0)>(S, o, d, t, st, C, false, top) >= 0;
   }
 };
 
@@ -104,43 +105,59 @@ __device__ V3 pathDisneyUniform(T& tr, const Env& env, Hit hit, int maxBounce, u
 }
 
 // pathTracingImportanceSampling IS:761-841
+//
+// Evaluated in a different order from the reference, with the same operations
+// on the same values (so the same bits): everything that needs the hit's
+// material -- the light sample's contribution and the BRDF sample with its
+// f_r and pdf -- is computed before either ray of the bounce is traced, and
+// the light contribution is added only if the shadow ray is unoccluded. No
+// material, view vector or normal is live across a traversal, which keeps the
+// kernel's register peak near the traversal's own. Random numbers are drawn
+// in the reference's order (r1, r2, then xi_3); the shadow ray is traced and
+// counted exactly when the reference traces it.
 template <class T>
 __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& seed, int px, int py,
                       uint32_t frameCounter, Counters& C, bool count) {
   V3 Lo = v3(0, 0, 0), history = v3(1, 1, 1);
   const uint32_t gi = grayCode(frameCounter + 1u);  // frameCounter = the sample index here
+  float cpu, cpv;
+  cranleyPattersonShift(px, py, cpu, cpv);
   for (int bounce = 0; bounce < maxBounce; bounce++) {
-    V3 V = -hit.viewDir;
-    V3 N = hit.N;
-    float r1 = randf(seed);
-    float r2 = randf(seed);
-    V3 Ldir = sampleHdrDir(env, r1, r2);
+    const V3 V = -hit.viewDir;
+    const V3 N = hit.N;
+    // (1) light sample IS:772-789
+    const float r1 = randf(seed);
+    const float r2 = randf(seed);
+    const V3 Ldir = sampleHdrDir(env, r1, r2);
     if (count) C.texels++;
-    if (dot(N, Ldir) > 0.0f) {
-      if (!tr.occluded(hit.P, Ldir)) {
-        V3 L = Ldir;
-        V3 color;
-        float pdf_light;
-        hdrColorPdf(env, L, color, pdf_light);
-        if (count) C.texels += 2;
-        V3 f_r = brdfIso(V, N, L, hit.m);
-        float pdf_brdf = brdfPdf(V, N, L, hit.m);
-        float mis_weight = misWeight(pdf_light, pdf_brdf);
-        V3 c = ((history * mis_weight) * color) * f_r;
-        Lo = Lo + (c * dot(N, L)) / pdf_light;
-      }
+    const bool tryLight = dot(N, Ldir) > 0.0f;
+    V3 lightC = v3(0, 0, 0);
+    if (tryLight) {
+      V3 color;
+      float pdf_light;
+      hdrColorPdf(env, Ldir, color, pdf_light);
+      V3 f_r = brdfIso(V, N, Ldir, hit.m);
+      float pdf_brdf = brdfPdf(V, N, Ldir, hit.m);
+      float mis_weight = misWeight(pdf_light, pdf_brdf);
+      V3 c = ((history * mis_weight) * color) * f_r;
+      lightC = (c * dot(N, Ldir)) / pdf_light;
     }
+    // (2) BRDF sample IS:791-840
     float u = sobolf(2u * (uint32_t)bounce, gi);
     float v = sobolf(2u * (uint32_t)bounce + 1u, gi);
-    cranleyPatterson(px, py, u, v);
-    float xi_3 = randf(seed);
-    V3 L = sampleBRDF(u, v, xi_3, V, N, hit.m);
-    float NdotL = dot(N, L);
+    cranleyPattersonApply(cpu, cpv, u, v);
+    const float xi_3 = randf(seed);
+    const V3 L = sampleBRDF(u, v, xi_3, V, N, hit.m);
+    const float NdotL = dot(N, L);
+    const V3 f_r = brdfIso(V, N, L, hit.m);
+    const float pdf_brdf = brdfPdf(V, N, L, hit.m);
+    if (tryLight && !tr.occluded(hit.P, Ldir)) {
+      Lo = Lo + lightC;
+      if (count) C.texels += 2;
+    }
     if (NdotL <= 0.0f) break;
     Hit nh;
     bool isHit = tr.closest(hit.P, L, nh);
-    V3 f_r = brdfIso(V, N, L, hit.m);
-    float pdf_brdf = brdfPdf(V, N, L, hit.m);
     if (pdf_brdf <= 0.0f) break;
     if (!isHit) {
       V3 color;
@@ -162,8 +179,9 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
 
 // main IS:844-872 for one pixel (px, py from the bottom-left)
 template <int INTEG, bool CULL, bool COUNT>
-__device__ __forceinline__ void shadePixel(const RenderParams& p, int px, int py, Stack& st, Counters& C) {
-  Tracer<CULL, COUNT> tr{p.scene, st, C};
+__device__ __forceinline__ void shadePixel(const RenderParams& p, int px, int py, Stack& st, Counters& C,
+                                           const float4* top) {
+  Tracer<CULL, COUNT> tr{p.scene, st, C, top};
   const int W = p.width, H = p.height;
   uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.sampleIndex * 26699u) | 1u;
   float pixx = (float)(2 * px + 1) / (float)W - 1.0f;
@@ -409,6 +427,15 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
   st.lds = s_stack + threadIdx.x;
   st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * p.ovfDepth : nullptr;
   st.sp = 0;
+  // the top of the tree (every ray's first node visits) staged in LDS once per block
+#if PT_LDS_NODES > 0
+  __shared__ float4 s_nodes[LDS_NODES * 4];
+  for (int i = threadIdx.x; i < p.scene.nTop * 4; i += BLOCK) s_nodes[i] = p.scene.bvh[i];
+  __syncthreads();
+  const float4* top = s_nodes;
+#else
+  const float4* top = nullptr;
+#endif
   Counters C = {0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   const int home = blockIdx.x & (NUM_QUEUES - 1);
@@ -424,7 +451,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
     const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
     const int px = gx * p.shardSize + (s % sub) * 8 + (lane & 7);
     const int py = gy * p.shardSize + (s / sub) * 8 + (lane >> 3);
-    if (px < p.width && py < p.height) shadePixel<INTEG, CULL, COUNT>(p, px, py, st, C);
+    if (px < p.width && py < p.height) shadePixel<INTEG, CULL, COUNT>(p, px, py, st, C, top);
     if (!COUNT && p.tileCost && lane == 0) p.tileCost[w] = (int)min(clock64() - t0, (long long)0x7fffffff);
   }
   addRays(p.rayShards, C.rays);

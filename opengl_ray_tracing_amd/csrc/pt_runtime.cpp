@@ -38,6 +38,7 @@ struct pt_ctx {
   float4* d_geo = nullptr;
   float* d_attr = nullptr;
   float4* d_bvh = nullptr;
+  int nDevNodes = 0;  // internal nodes in d_bvh (device ids 0..nDevNodes-1)
   int rootRef = REF_NONE;
   int nTri = 0, nNodes = 0, depth = 0, maxStack = 0;
   // env
@@ -217,6 +218,47 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
   }
   // node references (ivec3(texelFetch) truncation, pass1.fsh:238-243)
   auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
+  auto isInternal = [&](int k) { return k > 0 && k < nNodes && nodeN(k) <= 0; };
+  // depth of the reachable tree (bounds the traversal stack; rejects cycles)
+  int depth = 0;
+  {
+    std::vector<std::pair<int, int>> st{{1, 1}};
+    long visits = 0;
+    while (!st.empty()) {
+      auto [k, d] = st.back();
+      st.pop_back();
+      if (++visits > 2L * nNodes) return fail(ctx, PT_E_BADSCENE, "node graph is not a tree (cycle)");
+      depth = std::max(depth, d);
+      if (nodeN(k) > 0) continue;
+      int L = (int)nodes[(size_t)k * 12 + 0], R = (int)nodes[(size_t)k * 12 + 1];
+      if (L > 0 && L < nNodes) st.push_back({L, d + 1});
+      if (R > 0 && R < nNodes) st.push_back({R, d + 1});
+    }
+  }
+  // Device ids of the reachable internal nodes: the first LDS_NODES in
+  // breadth-first order from the root (the top of the tree, which every ray
+  // walks: the megakernel stages exactly these ids in LDS), the rest in the
+  // reference's id order (its preorder, which keeps subtrees together). Only
+  // the storage order changes; traversal visits the same nodes in the same
+  // order.
+  std::vector<int> newId(nNodes, -1), order;
+  {
+    std::vector<char> reach(nNodes, 0);
+    std::vector<int> bfs;
+    if (isInternal(1)) { bfs.push_back(1); reach[1] = 1; }
+    for (size_t h = 0; h < bfs.size(); h++) {
+      const int k = bfs[h];
+      for (int c = 0; c < 2; c++) {
+        const int ch = (int)nodes[(size_t)k * 12 + c];
+        if (isInternal(ch) && !reach[ch]) { reach[ch] = 1; bfs.push_back(ch); }
+      }
+    }
+    for (size_t h = 0; h < bfs.size() && h < (size_t)LDS_NODES; h++) order.push_back(bfs[h]);
+    for (int k : order) newId[k] = -2;
+    for (int k = 1; k < nNodes; k++)
+      if (reach[k] && newId[k] == -1) order.push_back(k);
+    for (size_t i = 0; i < order.size(); i++) newId[order[i]] = (int)i;
+  }
   std::string bad;
   auto encodeRef = [&](int k) -> int {
     if (k <= 0 || k >= nNodes) return REF_NONE;
@@ -227,12 +269,12 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
       if (n > MAX_LEAF) { bad = "leaf larger than 32 triangles at node " + std::to_string(k); return REF_NONE; }
       return (int)~(((uint32_t)index << LEAF_CNT_BITS) | (uint32_t)(n - 1));
     }
-    return k;
+    return newId[k];
   };
-  std::vector<float4> bvh((size_t)nNodes * 4, make_float4(0, 0, 0, 0));
+  std::vector<float4> bvh(std::max<size_t>(order.size(), 1) * 4, make_float4(0, 0, 0, 0));
   const float inf = INFINITY;
-  for (int k = 1; k < nNodes; k++) {
-    if (nodeN(k) > 0) continue;
+  for (size_t id = 0; id < order.size(); id++) {
+    const int k = order[id];
     int L = (int)nodes[(size_t)k * 12 + 0], R = (int)nodes[(size_t)k * 12 + 1];
     int lr = encodeRef(L), rr = encodeRef(R);
     if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
@@ -250,29 +292,13 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
     float refs[2];
     std::memcpy(&refs[0], &lr, 4);
     std::memcpy(&refs[1], &rr, 4);
-    bvh[4 * (size_t)k + 0] = make_float4(la.x, ra.x, la.y, ra.y);
-    bvh[4 * (size_t)k + 1] = make_float4(la.z, ra.z, lb.x, rb.x);
-    bvh[4 * (size_t)k + 2] = make_float4(lb.y, rb.y, lb.z, rb.z);
-    bvh[4 * (size_t)k + 3] = make_float4(refs[0], refs[1], 0.0f, 0.0f);
+    bvh[4 * id + 0] = make_float4(la.x, ra.x, la.y, ra.y);
+    bvh[4 * id + 1] = make_float4(la.z, ra.z, lb.x, rb.x);
+    bvh[4 * id + 2] = make_float4(lb.y, rb.y, lb.z, rb.z);
+    bvh[4 * id + 3] = make_float4(refs[0], refs[1], 0.0f, 0.0f);
   }
   int rootRef = encodeRef(1);
   if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
-  // depth of the reachable tree (bounds the traversal stack)
-  int depth = 0;
-  {
-    std::vector<std::pair<int, int>> st{{1, 1}};
-    long visits = 0;
-    while (!st.empty()) {
-      auto [k, d] = st.back();
-      st.pop_back();
-      if (++visits > 2L * nNodes) return fail(ctx, PT_E_BADSCENE, "node graph is not a tree (cycle)");
-      depth = std::max(depth, d);
-      if (nodeN(k) > 0) continue;
-      int L = (int)nodes[(size_t)k * 12 + 0], R = (int)nodes[(size_t)k * 12 + 1];
-      if (L > 0 && L < nNodes) st.push_back({L, d + 1});
-      if (R > 0 && R < nNodes) st.push_back({R, d + 1});
-    }
-  }
   dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh);
   CK(hipMalloc(&ctx->d_geo, geo.size() * sizeof(float4)));
   CK(hipMalloc(&ctx->d_attr, (size_t)nTri * 36 * sizeof(float)));
@@ -282,6 +308,7 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
   CK(hipMemcpy(ctx->d_bvh, bvh.data(), bvh.size() * sizeof(float4), hipMemcpyHostToDevice));
   ctx->nTri = nTri;
   ctx->nNodes = nNodes;
+  ctx->nDevNodes = (int)order.size();
   ctx->rootRef = rootRef;
   ctx->depth = depth;
   ctx->maxStack = depth + 1;
@@ -399,6 +426,7 @@ static SceneView sceneView(const pt_ctx* ctx) {
   s.geo = ctx->d_geo;
   s.attr = ctx->d_attr;
   s.bvh = ctx->d_bvh;
+  s.nTop = std::min(LDS_NODES, ctx->nDevNodes);
   s.rootRef = ctx->rootRef;
   s.nTri = ctx->nTri;
   return s;

@@ -67,6 +67,13 @@ struct NodeHit {
 };
 __device__ __forceinline__ void visitNode(const float4* nd, V3 o, V3 inv, NodeHit& h) {
   const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+#ifdef PT_SCALAR_SLAB
+  h.d1 = hitAABB(o, inv, make_float4(q0.x, q0.z, q1.x, 0), make_float4(q1.z, q2.x, q2.z, 0), h.t0l);
+  h.d2 = hitAABB(o, inv, make_float4(q0.y, q0.w, q1.y, 0), make_float4(q1.w, q2.y, q2.w, 0), h.t0r);
+  h.lref = __float_as_int(q3.x);
+  h.rref = __float_as_int(q3.y);
+  return;
+#endif
   const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
   const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
   const f32x2 lox = {q0.x, q0.y}, loy = {q0.z, q0.w}, loz = {q1.x, q1.y};
@@ -130,9 +137,13 @@ __device__ __forceinline__ bool isLeafRef(int ref) { return ref < 0 && ref != RE
 // in the reference's order (the parked leaf precedes every node visited
 // speculatively); node visits use a possibly stale tbest for culling, which
 // only culls less.
-template <bool ANYHIT, bool CULL, bool COUNT, class StackType>
+//
+// top (LDSTOP): the LDS copy of device node ids [0, S.nTop) -- the top of the
+// tree -- read in place of the global records (one flat load serves lanes in
+// both address spaces).
+template <bool ANYHIT, bool CULL, bool COUNT, class StackType, bool LDSTOP = false>
 __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
-                                        bool anyRT = false) {
+                                        bool anyRT = false, const float4* top = nullptr) {
   V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float tbest = PT_INF;
   int best = -1;
@@ -144,7 +155,9 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
     // node phase
     while (ref >= 0) {
       NodeHit nh;
-      visitNode(S.bvh + 4 * (size_t)ref, o, inv, nh);
+      const float4* nd = S.bvh + 4 * (size_t)ref;
+      if (LDSTOP && ref < S.nTop) nd = top + 4 * ref;
+      visitNode(nd, o, inv, nh);
       const int lref = nh.lref, rref = nh.rref;
       const float d1 = nh.d1, d2 = nh.d2, t0l = nh.t0l, t0r = nh.t0r;
       bool h1 = (lref != REF_NONE) && d1 > 0.0f;
@@ -190,6 +203,24 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
       // two triangles per iteration, their eight records fetched together (one
       // memory round trip per pair; the geometry buffer carries one zero record
       // past the last triangle); tested in index order with the running tbest
+#ifdef PT_TRI_SINGLE
+      for (int k = 0; k < cnt; k++) {
+        const int i = start + k;
+        const float4* g = S.geo + 4 * (size_t)i;
+        float t0;
+        if (COUNT) {
+          bool h0 = triTest(g[0], g[1], g[2], g[3], o, d, PT_INF, t0);
+          C.tris++;
+          if (h0 && t0 < localBest) { localBest = t0; C.mats++; }
+          if (h0 && t0 < tbest) { tbest = t0; best = i; }
+        } else if (triTest(g[0], g[1], g[2], g[3], o, d, tbest, t0)) {
+          tbest = t0;
+          best = i;
+          if (ANYHIT || anyRT) { tOut = tbest; return best; }
+        }
+      }
+      if (false)
+#endif
       for (int k = 0; k < cnt; k += 2) {
         const int i = start + k;
         const float4* g = S.geo + 4 * (size_t)i;

@@ -2,6 +2,7 @@
 """A/B timing of in-tree tuning builds of libpt.so (opengl_ray_tracing_amd/_variants/).
 
     python tools/tune.py --build w4:PT_MIN_WAVES=4 w5:PT_MIN_WAVES=5   # here (cross-compiles)
+    python tools/tune.py --build noslp:+-fno-slp-vectorize             # "+flag" = extra hipcc flag
     python tools/tune.py --variants base w4 w5 --config c2 --rounds 3 # on the GPU box
 
 Each measurement runs in its own process (one library per process); variants
@@ -65,8 +66,10 @@ def main():
         from opengl_ray_tracing_amd import _build
         for spec in a.build:
             name, _, defs = spec.partition(":")
-            d = dict(kv.split("=") for kv in defs.split(",") if kv)
-            print("built", _build.build_variant(name, d))
+            items = [kv for kv in defs.split(",") if kv]
+            d = dict(kv.split("=", 1) for kv in items if not kv.startswith("+"))
+            flags = [kv[1:] for kv in items if kv.startswith("+")]  # "+-fno-slp-vectorize": an extra hipcc flag
+            print("built", _build.build_variant(name, d, flags))
         return
     keys = [(v, f) for v in a.variants for f in a.flags]
     res = {k: [] for k in keys}
