@@ -138,7 +138,8 @@ __device__ __forceinline__ Material loadMaterial(const float* rec) {
 }
 
 // ------------------------------------------------------------ environment
-__device__ __forceinline__ float4 texNearest(const float4* img, int w, int h, float u, float v) {
+template <class T>
+__device__ __forceinline__ T texNearest(const T* img, int w, int h, float u, float v) {
   float fx = floorf(u * (float)w);
   float fy = floorf(v * (float)h);
   fx = fminf(fmaxf(fx, 0.0f), (float)(w - 1));
@@ -176,7 +177,7 @@ __device__ __forceinline__ V3 hdrColor(const Env& e, V3 L) {
 __device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
   float x = 0.0f, y = 0.0f;
   if (e.cache) {
-    float4 c = texNearest(e.cache, e.w, e.h, xi1, xi2);
+    float2 c = texNearest(e.cache, e.w, e.h, xi1, xi2);
     x = c.x;
     y = c.y;
   }
@@ -192,7 +193,7 @@ __device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
 __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
   float u, w;
   toSpherical(normalize(L), u, w);
-  float pdf = e.cache ? texNearest(e.cache, e.w, e.h, u, w).z : 0.0f;
+  float pdf = e.hdr ? texNearest(e.hdr, e.w, e.h, u, w).w : 0.0f;
   float theta = PT_PI * (0.5f - w);
   float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
   float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
@@ -202,16 +203,11 @@ __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
 // hdrColor(L) and hdrPdf(L) of the same direction (every MIS use pairs them):
 // one toSphericalCoord, the same operations and results as the two calls.
 __device__ __forceinline__ void hdrColorPdf(const Env& e, V3 L, V3& color, float& pdf) {
-  if (!e.hdr) {
-    color = v3(0, 0, 0);
-  }
   float u, w;
   toSpherical(normalize(L), u, w);
-  if (e.hdr) {
-    float4 c = texNearest(e.hdr, e.w, e.h, u, w);
-    color = v3(c.x, c.y, c.z);
-  }
-  const float p = e.cache ? texNearest(e.cache, e.w, e.h, u, w).z : 0.0f;
+  const float4 c = e.hdr ? texNearest(e.hdr, e.w, e.h, u, w) : make_float4(0, 0, 0, 0);
+  color = v3(c.x, c.y, c.z);
+  const float p = c.w;  // the cache pdf of the same texel
   const float theta = PT_PI * (0.5f - w);
   const float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
   const float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);

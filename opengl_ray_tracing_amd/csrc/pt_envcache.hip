@@ -96,6 +96,21 @@ __global__ void hdrSampleKernel(const float* pdf, const float* cdfX, const float
 }
 
 // scratch: 2*w*h + 2*w + 1 floats
+// render layout of an env map (pt_kernels.h Env): the pdf (cache.z) joins the
+// texel's colour, the sampling table keeps (x, y)
+__global__ void envPackKernel(float4* hdr, const float4* cache, float2* samp, int n) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float4 c = cache[k];
+  hdr[k].w = c.z;
+  samp[k] = make_float2(c.x, c.y);
+}
+
+hipError_t launchEnvPack(float4* hdr, const float4* cache, float2* samp, int n, hipStream_t s) {
+  hipLaunchKernelGGL(envPackKernel, dim3((n + 255) / 256), dim3(256), 0, s, hdr, cache, samp, n);
+  return hipGetLastError();
+}
+
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s) {
   const int n = w * h;
   float* pdf = scratch;

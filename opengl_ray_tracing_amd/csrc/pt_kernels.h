@@ -53,9 +53,11 @@ struct SceneView {
 };
 
 // HDR environment (hdrMap + hdrCache textures, IS main.cpp:843-853), float4 texels
+// Render layout: one 16-byte texel serves hdrColor and hdrPdf of a direction
+// together (every MIS lookup pairs them), so a miss costs one line, not two.
 struct Env {
-  const float4* hdr;    // w x h, rgb in xyz (row 0 = first scanline); null = black
-  const float4* cache;  // calculateHdrCache: (x, y, pdf); null = none
+  const float4* hdr;    // w x h: (r, g, b, calculateHdrCache pdf) (row 0 = first scanline); null = black
+  const float2* cache;  // calculateHdrCache sample table (x, y); null exactly when hdr is null
   int w, h, res;        // res = hdrResolution
 };
 
@@ -112,6 +114,8 @@ struct PackParams {
 
 // calculateHdrCache on the device (pt_envcache.hip); scratch: 2*w*h + 2*w + 1 floats
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);
+// hdr[k].w = cache[k].z, samp[k] = cache[k].xy (the Env render layout)
+hipError_t launchEnvPack(float4* hdr, const float4* cache, float2* samp, int n, hipStream_t s);
 hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count);
 // tile order of the next frame: each queue band's groups of `group` consecutive
 // tiles sorted by this frame's summed cost, descending (tiles inside a group keep

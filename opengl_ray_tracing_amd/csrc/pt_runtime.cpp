@@ -43,7 +43,7 @@ struct pt_ctx {
   int nTri = 0, nNodes = 0, depth = 0, maxStack = 0;
   // env
   float4* d_hdr = nullptr;
-  float4* d_cache = nullptr;
+  float2* d_cache = nullptr;  // sample table (x, y); the pdf lives in d_hdr[k].w
   int hdrW = 0, hdrH = 0;
   // BASIC shapes
   float* d_shapes = nullptr;
@@ -343,16 +343,27 @@ int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
   if (!hdr) return PT_OK;
   if (w <= 0 || h <= 0) return PT_E_INVALID;
   const size_t n = (size_t)w * h;
+  // render layout (pt_kernels.h Env): (r, g, b, pdf) texels + (x, y) sample table
   std::vector<float4> a(n);
-  for (size_t k = 0; k < n; k++) a[k] = make_float4(hdr[3 * k], hdr[3 * k + 1], hdr[3 * k + 2], 0.0f);
+  for (size_t k = 0; k < n; k++)
+    a[k] = make_float4(hdr[3 * k], hdr[3 * k + 1], hdr[3 * k + 2], cache ? cache[3 * k + 2] : 0.0f);
   CK(hipMalloc(&ctx->d_hdr, n * sizeof(float4)));
-  CK(hipMalloc(&ctx->d_cache, n * sizeof(float4)));
+  CK(hipMalloc(&ctx->d_cache, n * sizeof(float2)));
   CK(hipMemcpy(ctx->d_hdr, a.data(), n * sizeof(float4), hipMemcpyHostToDevice));
   if (cache) {
-    for (size_t k = 0; k < n; k++) a[k] = make_float4(cache[3 * k], cache[3 * k + 1], cache[3 * k + 2], 0.0f);
-    CK(hipMemcpy(ctx->d_cache, a.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    std::vector<float2> b(n);
+    for (size_t k = 0; k < n; k++) b[k] = make_float2(cache[3 * k], cache[3 * k + 1]);
+    CK(hipMemcpy(ctx->d_cache, b.data(), n * sizeof(float2), hipMemcpyHostToDevice));
   } else {
-    int rc = deviceHdrCache(ctx, hdr, w, h, ctx->d_cache);  // calculateHdrCache on the GPU
+    float4* full = nullptr;  // calculateHdrCache on the GPU, then packed into the render layout
+    CK(hipMalloc(&full, n * sizeof(float4)));
+    int rc = deviceHdrCache(ctx, hdr, w, h, full);
+    if (!rc) {
+      hipError_t e = launchEnvPack(ctx->d_hdr, full, ctx->d_cache, (int)n, ctx->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+      if (e != hipSuccess) rc = fail(ctx, PT_E_HIP, std::string("env pack: ") + hipGetErrorString(e));
+    }
+    (void)hipFree(full);
     if (rc) return rc;
   }
   ctx->hdrW = w;
