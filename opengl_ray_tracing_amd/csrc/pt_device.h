@@ -138,6 +138,40 @@ __device__ __forceinline__ Material loadMaterial(const float* rec) {
 }
 
 // ------------------------------------------------------------ environment
+// Streaming (non-temporal) loads and stores for the env map and the
+// accumulation buffer: their lines are touched about once per frame, so they
+// are marked to leave L2 first and not evict the BVH and triangle lines every
+// traversal re-reads (PT_NT_STREAM=0: plain accesses).
+#ifndef PT_NT_STREAM
+#define PT_NT_STREAM 1
+#endif
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ldStream(const float4* p) {
+#if PT_NT_STREAM
+  const f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ float2 ldStream(const float2* p) {
+#if PT_NT_STREAM
+  const f32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x2_t*>(p));
+  return make_float2(v.x, v.y);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void stStream(float4* p, float4 v) {
+#if PT_NT_STREAM
+  const f32x4_t x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<f32x4_t*>(p));
+#else
+  *p = v;
+#endif
+}
+
 template <class T>
 __device__ __forceinline__ T texNearest(const T* img, int w, int h, float u, float v) {
   float fx = floorf(u * (float)w);
@@ -145,7 +179,7 @@ __device__ __forceinline__ T texNearest(const T* img, int w, int h, float u, flo
   fx = fminf(fmaxf(fx, 0.0f), (float)(w - 1));
   fy = fminf(fmaxf(fy, 0.0f), (float)(h - 1));
   int x = (int)fx, y = (int)fy;
-  return img[y * w + x];
+  return ldStream(img + y * w + x);
 }
 // SampleSphericalMap IS:175-181 / toSphericalCoord IS:638-644
 __device__ __forceinline__ void toSpherical(V3 v, float& u, float& w) {

@@ -18,10 +18,20 @@ constexpr int BLOCK = 256;        // 4 waves of 64
 #endif
 constexpr int LDS_STACK = PT_LDS_STACK;
 #ifndef PT_LDS_NODES
-#define PT_LDS_NODES 256
+#define PT_LDS_NODES 128
 #endif
 // top-of-tree nodes (breadth-first from the root) the megakernel keeps in LDS, 64 B each
-constexpr int LDS_NODES = PT_LDS_NODES;  // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
+constexpr int LDS_NODES = PT_LDS_NODES;
+#ifndef PT_SPLIT_PCT
+#define PT_SPLIT_PCT 25  // megakernel: split a tile whose longest item costs more than this % of a wave's share
+#endif
+#ifndef PT_SPLIT_AUTO
+#define PT_SPLIT_AUTO 1  // the runtime measures split vs unsplit after each running-mean restart (splitPolicy)
+#endif
+#ifndef PT_WAVE_TRACE
+#define PT_WAVE_TRACE 0  // diagnostics build: record each megakernel wave's lifetime (tools/wave_trace.py)
+#endif
+ // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
 #ifndef PT_NUM_QUEUES
 #define PT_NUM_QUEUES 32
 #endif
@@ -82,8 +92,12 @@ struct RenderParams {
   int ovfDepth;
   unsigned long long* stats;  // [rays, nodes, tris, mats, texels]
   unsigned long long* rayShards;  // RAY_SHARDS ray counters (stride RAY_SHARD_STRIDE)
-  const int* tileOrder; // per-band tile order (null = identity), see reorderKernel
-  int* tileCost;        // per-tile cost of this frame (shader cycles), null = not recorded
+  const int* tileOrder; // per-band work items (null = one per tile, in id order), then NUM_QUEUES item
+                        // counts; see TileCursor / reorderKernel
+  int orderCap;         // entries per band in tileOrder
+  int* tileCost;        // per tile: summed cost of its items this frame (shader cycles), null = not recorded
+  int* tileCostMax;     // per tile: its longest item this frame
+  unsigned long long* waveTrace;  // PT_WAVE_TRACE builds only: 6 u64 per wave (pt_runtime.cpp, tools/wave_trace.py)
 };
 
 struct TraceParams {
@@ -121,7 +135,10 @@ hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStre
 // tiles sorted by this frame's summed cost, descending (tiles inside a group keep
 // their order, which keeps neighbouring tiles together for the caches)
 constexpr int REORDER_MAX = 4096;  // most groups per band the one-block LDS sort handles
-hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, int group, hipStream_t s);
+// order: NUM_QUEUES * orderCap items, then NUM_QUEUES item counts; cost / costMax are read
+// and zeroed; splitLg (one per tile) is the split state carried from frame to frame
+hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* order, int perQueue, int orderCap,
+                         int numItems, int group, int numWaves, int splitPct, hipStream_t s);
 hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, int* nb);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull);
 hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb);

@@ -177,13 +177,12 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
   return Lo;
 }
 
-// main IS:844-872 for one pixel (px, py from the bottom-left)
-template <int INTEG, bool CULL, bool COUNT>
-__device__ __forceinline__ void shadePixel(const RenderParams& p, int px, int py, Stack& st, Counters& C,
-                                           const float4* top) {
-  Tracer<CULL, COUNT> tr{p.scene, st, C, top};
+// main IS:844-872 for one pixel (px, py from the bottom-left), in two parts:
+// the camera ray (cameraRay + primaryPixel) and the rest of the path
+// (finishPixel, which recomputes the camera ray and RNG state from the pixel).
+__device__ __forceinline__ V3 cameraRay(const RenderParams& p, int px, int py, uint32_t& seed) {
   const int W = p.width, H = p.height;
-  uint32_t seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.sampleIndex * 26699u) | 1u;
+  seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.sampleIndex * 26699u) | 1u;
   float pixx = (float)(2 * px + 1) / (float)W - 1.0f;
   float pixy = (float)(2 * py + 1) / (float)H - 1.0f;
   float ax = (randf(seed) - 0.5f) / (float)W;
@@ -192,25 +191,48 @@ __device__ __forceinline__ void shadePixel(const RenderParams& p, int px, int py
   const float* M = p.cam;
   V3 c0 = v3(M[0], M[1], M[2]), c1 = v3(M[4], M[5], M[6]), c2 = v3(M[8], M[9], M[10]), c3 = v3(M[12], M[13], M[14]);
   V3 dir = (c0 * x + c1 * y) + (c2 * z + c3 * 0.0f);
-  dir = normalize(dir);
-  V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-  Hit first;
-  V3 color;
-  if (!tr.closest(eye, dir, first)) {
-    color = sampleHdr(p.env, dir);
-    if (COUNT) C.texels++;
-  } else {
-    V3 Li;
-    if (INTEG == 0) Li = pathLambert(tr, p.env, first, p.maxBounce, seed, C, COUNT);
-    else if (INTEG == 1) Li = pathDisneyUniform(tr, p.env, first, p.maxBounce, seed, C, COUNT);
-    else Li = pathMIS(tr, p.env, first, p.maxBounce, seed, px, py, p.sampleIndex, C, COUNT);
-    color = first.m.emissive + Li;
-  }
-  float4* a = p.accum + (size_t)py * W + px;
-  float4 old = *a;
-  if (COUNT) C.texels++;
+  return normalize(dir);
+}
+
+__device__ __forceinline__ void accumulate(const RenderParams& p, int px, int py, V3 color, Counters& C, bool count) {
+  float4* a = p.accum + (size_t)py * p.width + px;
+  float4 old = ldStream(a);
+  if (count) C.texels++;
   float w = 1.0f / (float)(p.frameCounter + 1u);
-  *a = make_float4(mixf(old.x, color.x, w), mixf(old.y, color.y, w), mixf(old.z, color.z, w), 1.0f);
+  stStream(a, make_float4(mixf(old.x, color.x, w), mixf(old.y, color.y, w), mixf(old.z, color.z, w), 1.0f));
+}
+
+// the camera ray's closest hit; a miss is finished here (sky colour accumulated)
+template <bool CULL, bool COUNT>
+__device__ __forceinline__ int primaryPixel(const RenderParams& p, int px, int py, Stack& st, Counters& C,
+                                            const float4* top, float& t) {
+  uint32_t seed;
+  const V3 dir = cameraRay(p, px, py, seed);
+  const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+  const int tri = traceRay<false, CULL, COUNT, Stack, (LDS_NODES > 0)>(p.scene, eye, dir, t, st, C, false, top);
+  if (tri < 0) {
+    const V3 color = sampleHdr(p.env, dir);
+    if (COUNT) C.texels++;
+    accumulate(p, px, py, color, C, COUNT);
+  }
+  return tri;
+}
+
+// the rest of the path of a pixel whose camera ray hit triangle tri at t
+template <int INTEG, bool CULL, bool COUNT>
+__device__ __forceinline__ void finishPixel(const RenderParams& p, int px, int py, int tri, float t, Stack& st,
+                                            Counters& C, const float4* top) {
+  Tracer<CULL, COUNT> tr{p.scene, st, C, top};
+  uint32_t seed;
+  const V3 dir = cameraRay(p, px, py, seed);  // the same ray and RNG state as primaryPixel
+  const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+  Hit first;
+  finishHit(p.scene, tri, eye, dir, t, first);
+  V3 Li;
+  if (INTEG == 0) Li = pathLambert(tr, p.env, first, p.maxBounce, seed, C, COUNT);
+  else if (INTEG == 1) Li = pathDisneyUniform(tr, p.env, first, p.maxBounce, seed, C, COUNT);
+  else Li = pathMIS(tr, p.env, first, p.maxBounce, seed, px, py, p.sampleIndex, C, COUNT);
+  accumulate(p, px, py, first.m.emissive + Li, C, COUNT);
 }
 
 // ------------------------------------------------ BASIC (BasicRayTracingWithC++)
@@ -354,28 +376,65 @@ __global__ __launch_bounds__(BLOCK) void basicKernel(BasicParams p) {
 }
 
 // ------------------------------------------------------------ tile order
-// One block per queue band: sort the band's tiles by the cost the megakernel
-// measured for them this frame (descending; ties by tile id), bitonic in LDS.
-// The next frame hands them out in that order (TileCursor), so the band's
-// long-path tiles start first. Progressive frames share camera and scene, so a
-// tile's cost is a good predictor of its cost in the next frame.
-__global__ __launch_bounds__(1024) void reorderKernel(const int* cost, int* order, int perQueue, int numItems,
-                                                       int group) {
+// One block per queue band, between frames: build the next frame's work items
+// (TileCursor) from the costs the megakernel measured in this one.
+//  * Split state: a wave runs its item's paths in lock step, so a tile whose
+//    lanes take turns at long traversals lasts the sum of its slowest lanes --
+//    for a few tiles most of a frame. A tile whose longest item cost more than
+//    splitPct % of a wave's share of the band (band cost / waves per band)
+//    is split once more (2^lg items of 64 >> lg pixels, lg <= 6); one whose
+//    items became cheap (< 1/4 of that) is merged back one step.
+//  * Order: items sorted by their tile's longest item, descending (ties by tile
+//    id; bitonic in LDS), so the long ones start first. Progressive frames share
+//    camera and scene, so this frame's costs predict the next frame's.
+// group > 1 sorts groups of consecutive tiles by summed cost and never splits.
+__global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, int* splitLg, int* order, int perQueue,
+                                                       int orderCap, int numItems, int group, int numWaves,
+                                                       int splitPct) {
   __shared__ unsigned long long key[REORDER_MAX];
+  __shared__ int scan[1024];
   __shared__ int partialPos;
+  __shared__ unsigned long long sumCost;
   const int q = blockIdx.x;
   const int base = q * perQueue;
   const int n = max(0, min(perQueue, numItems - base));
   const int ng = (n + group - 1) / group;  // groups of `group` consecutive tiles (the last may be short)
   const int lastSize = n - (ng - 1) * group;
+  const bool splitting = group == 1 && splitLg != nullptr && splitPct > 0;
   int size = 1;
   while (size < ng) size <<= 1;
+  if (threadIdx.x == 0) sumCost = 0;
+  __syncthreads();
+  unsigned long long mySum = 0;
+  for (int g = threadIdx.x; g < ng; g += blockDim.x) {
+    const int t0 = base + g * group, t1 = min(t0 + group, base + n);
+    for (int t = t0; t < t1; t++) mySum += (unsigned)max(cost[t], 0);
+  }
+  atomicAdd(&sumCost, mySum);
+  __syncthreads();
+  // a wave's share of the band's work: the cost above which an item forms the tail
+  const unsigned long long share = sumCost / (unsigned long long)max(1, numWaves / NUM_QUEUES);
+  const unsigned long long target = max(share * (unsigned long long)splitPct / 100ull, 1ull);
   for (int g = threadIdx.x; g < size; g += blockDim.x) {
     unsigned long long k = 0;  // padding sorts last
     if (g < ng) {
       unsigned long long c = 0;
       const int t0 = base + g * group, t1 = min(t0 + group, base + n);
-      for (int t = t0; t < t1; t++) c += (unsigned)max(cost[t], 1);
+      if (splitting) {
+        const int t = t0;
+        const unsigned long long m = (unsigned)max(costMax[t], 1);
+        int lg = splitLg[t];
+        if (m > target && lg < MAX_SPLIT_LG) lg++;
+        else if (lg > 0 && 4 * m < target) lg--;
+        splitLg[t] = lg;
+        c = m;
+        costMax[t] = 0;
+      } else {
+        for (int t = t0; t < t1; t++) c += (unsigned)max(cost[t], 1);
+        if (costMax)
+          for (int t = t0; t < t1; t++) costMax[t] = 0;
+      }
+      for (int t = t0; t < t1; t++) cost[t] = 0;
       k = (min(c, 0xffffffffull) << 32) | (unsigned)(0x7fffffff - g);
     }
     key[g] = k;
@@ -397,6 +456,35 @@ __global__ __launch_bounds__(1024) void reorderKernel(const int* cost, int* orde
       __syncthreads();
     }
   }
+  int* out = order + (size_t)q * orderCap;
+  if (splitting) {
+    // item offsets: exclusive scan of 2^lg over the sorted ranks (4 ranks per thread)
+    const int per = (ng + 1023) / 1024;
+    const int r0 = min(ng, (int)threadIdx.x * per), r1 = min(ng, r0 + per);
+    int local = 0;
+    for (int r = r0; r < r1; r++) local += 1 << splitLg[base + 0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu)];
+    scan[threadIdx.x] = local;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int v = threadIdx.x >= (unsigned)off ? scan[threadIdx.x - off] : 0;
+      __syncthreads();
+      scan[threadIdx.x] += v;
+      __syncthreads();
+    }
+    const int total = scan[1023];
+    if (total <= orderCap) {
+      int pos = scan[threadIdx.x] - local;
+      for (int r = r0; r < r1; r++) {
+        const int t = base + 0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu);
+        const int lg = splitLg[t];
+        for (int sIdx = 0; sIdx < (1 << lg); sIdx++) out[pos++] = t | sIdx << ITEM_TILE_BITS | lg << 28;
+      }
+      if (threadIdx.x == 0) order[(size_t)NUM_QUEUES * orderCap + q] = total;
+      return;
+    }
+    // no room: this frame unsplit, and the band starts over
+    for (int r = threadIdx.x; r < ng; r += blockDim.x) splitLg[base + r] = 0;
+  }
   for (int r = threadIdx.x; r < ng; r += blockDim.x)
     if (0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu) == ng - 1) partialPos = r;
   __syncthreads();
@@ -404,13 +492,16 @@ __global__ __launch_bounds__(1024) void reorderKernel(const int* cost, int* orde
     const int g = 0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu);
     const int off = r * group - (r > partialPos ? group - lastSize : 0);
     const int len = g == ng - 1 ? lastSize : group;
-    for (int k = 0; k < len; k++) order[base + off + k] = base + g * group + k;
+    for (int k = 0; k < len; k++) out[off + k] = base + g * group + k;
   }
+  if (threadIdx.x == 0) order[(size_t)NUM_QUEUES * orderCap + q] = n;
 }
 
-hipError_t launchReorder(const int* cost, int* order, int perQueue, int numItems, int group, hipStream_t s) {
-  if ((perQueue + group - 1) / group > REORDER_MAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(reorderKernel, dim3(NUM_QUEUES), dim3(1024), 0, s, cost, order, perQueue, numItems, group);
+hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* order, int perQueue, int orderCap,
+                         int numItems, int group, int numWaves, int splitPct, hipStream_t s) {
+  if ((perQueue + group - 1) / group > REORDER_MAX || orderCap < perQueue) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(reorderKernel, dim3(NUM_QUEUES), dim3(1024), 0, s, cost, costMax, splitLg, order, perQueue,
+                     orderCap, numItems, group, numWaves, splitPct);
   return hipGetLastError();
 }
 
@@ -426,7 +517,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
   Stack st;
   st.lds = s_stack + threadIdx.x;
   st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * p.ovfDepth : nullptr;
-  st.sp = 0;
+  st.reset();
   // the top of the tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
   __shared__ float4 s_nodes[LDS_NODES * 4];
@@ -441,19 +532,67 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
   const int home = blockIdx.x & (NUM_QUEUES - 1);
   const int tilesPerShard = p.shardTiles;  // 8x8 wave tiles per shard tile
   const int sub = p.shardSize >> 3;        // wave tiles per shard-tile edge
+#if PT_WAVE_TRACE
+  const unsigned long long wStart = wall_clock64();
+  unsigned long long wTiles = 0, wLongest = 0, wLongestAt = 0, wNodeIt = 0, wLeafIt = 0;
+#endif
   TileCursor cur;
+  // Each lane runs its pixel's whole path right after the tile's camera rays.
+  // (Deferring the paths of the pixels that hit something to a per-wave LDS
+  // queue and running them 64 at a time keeps every lane busy, but it mixes
+  // tiles: 64-path batches made c2 0.77 ms instead of 0.55, 32-path batches
+  // 0.59 -- the coherence of one tile's rays is worth more than full lanes.)
   while (true) {
-    const int w = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder);
-    if (w < 0) break;
+    const int item = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+    if (item < 0) break;
+    const int w = itemTile(item);
     const long long t0 = COUNT ? 0 : clock64();
+#if PT_WAVE_TRACE
+    const unsigned long long tw0 = wall_clock64();
+    const uint32_t n0 = C.nodes, l0 = C.tris, m0 = C.mats;
+#endif
     const int j = w / tilesPerShard, s = w - j * tilesPerShard;
     const int g = j * p.world + p.rank;  // global shard tile id (row-major)
     const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
-    const int px = gx * p.shardSize + (s % sub) * 8 + (lane & 7);
-    const int py = gy * p.shardSize + (s / sub) * 8 + (lane >> 3);
-    if (px < p.width && py < p.height) shadePixel<INTEG, CULL, COUNT>(p, px, py, st, C, top);
-    if (!COUNT && p.tileCost && lane == 0) p.tileCost[w] = (int)min(clock64() - t0, (long long)0x7fffffff);
+    // a split item runs pixels [sub * n, (sub + 1) * n) of the tile (n = 64 >> lg), one per lane
+    const int lg = itemLg(item), nLanes = 64 >> lg;
+    const int k = itemSub(item) * nLanes + lane;
+    const int px = gx * p.shardSize + (s % sub) * 8 + (k & 7);
+    const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
+    if (lane < nLanes && px < p.width && py < p.height) {
+      float t;
+      const int tri = primaryPixel<CULL, COUNT>(p, px, py, st, C, top, t);
+      if (tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);
+    }
+    if (!COUNT && p.tileCost && lane == 0) {
+      const int dt = (int)min(clock64() - t0, (long long)0x3fffffff);
+      atomicAdd(p.tileCost + w, dt);
+      atomicMax(p.tileCostMax + w, dt);
+    }
+#if PT_WAVE_TRACE
+    const unsigned long long tEnd = wall_clock64();
+    wTiles++;
+    uint32_t dn = C.nodes - n0, dl = C.tris - l0, dw = C.mats - m0;
+    for (int off = 32; off > 0; off >>= 1) dw += (uint32_t)__shfl_xor(dw, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+      dn = max(dn, (uint32_t)__shfl_xor(dn, off, 64));
+      dl = max(dl, (uint32_t)__shfl_xor(dl, off, 64));
+    }
+    if (tEnd - tw0 > wLongest) {
+      wNodeIt = dn;
+      wLeafIt = dl | (unsigned long long)dw << 32;
+      wLongest = tEnd - tw0;
+      wLongestAt = (unsigned long long)__shfl(px, 0, 64) << 16 | (unsigned long long)__shfl(py, 0, 64);
+    }
+#endif
   }
+#if PT_WAVE_TRACE
+  if (p.waveTrace && lane == 0) {
+    unsigned long long* r = p.waveTrace + 6 * ((size_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
+    r[0] = wStart; r[1] = wall_clock64(); r[2] = wTiles | wLongestAt << 32; r[3] = wLongest;
+    r[4] = wNodeIt; r[5] = wLeafIt;
+  }
+#endif
   addRays(p.rayShards, C.rays);
   if (COUNT) {
     uint32_t n = waveSum(C.nodes), t = waveSum(C.tris), m = waveSum(C.mats), x = waveSum(C.texels);

@@ -60,9 +60,9 @@ struct PathState {
 
 __device__ __forceinline__ void writeAccum(const RenderParams& p, int px, int py, V3 color) {
   float4* a = p.accum + (size_t)py * p.width + px;
-  float4 old = *a;
+  float4 old = ldStream(a);
   float w = 1.0f / (float)(p.frameCounter + 1u);
-  *a = make_float4(mixf(old.x, color.x, w), mixf(old.y, color.y, w), mixf(old.z, color.z, w), 1.0f);
+  stStream(a, make_float4(mixf(old.x, color.x, w), mixf(old.y, color.y, w), mixf(old.z, color.z, w), 1.0f));
 }
 
 // main IS:846-850: seed and camera ray of pixel (px, py)
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
   StackT<REGEN_LDS_STACK, BLOCK> st;
   st.lds = s_stack + threadIdx.x;
   st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * p.ovfDepth : nullptr;
-  st.sp = 0;
+  st.reset();
   Counters C = {0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,6 +57,12 @@ struct pt_ctx {
   int* d_ovf = nullptr;
   int* d_cost = nullptr;   // per-tile cost of the last frame (megakernel)
   int* d_order = nullptr;  // per-band tile order for the next frame
+  // tile-split policy probe (splitPolicy): frames since the probe (re)started,
+  // the summed frame times of each policy, the decision
+  int probeFrame = 0, splitOnFrames = 0, splitOffFrames = 0;
+  double splitOnMs = 0.0, splitOffMs = 0.0;
+  int splitDecided = -1;   // -1 probing, 0 off, 1 on
+  int lastSplit = 0;       // the policy of the last reorder launch
   bool orderValid = false;
   size_t ovfInts = 0;
   // shards
@@ -112,7 +119,9 @@ const char* pt_last_error(pt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_creat
 int pt_create(pt_ctx** out, const pt_config* cfg) {
   if (!out || !cfg) return PT_E_INVALID;
   *out = nullptr;
-  if (cfg->width <= 0 || cfg->height <= 0 || cfg->integrator < 0 || cfg->integrator > PT_BASIC_CPU_COMPAT ||
+  // width, height < 65536: the megakernel packs a pixel as (px | py << 16)
+  if (cfg->width <= 0 || cfg->height <= 0 || cfg->width > 65535 || cfg->height > 65535 || cfg->integrator < 0 ||
+      cfg->integrator > PT_BASIC_CPU_COMPAT ||
       cfg->tile_world < 1 || cfg->tile_rank < 0 || cfg->tile_rank >= cfg->tile_world || cfg->sample_world < 0 ||
       cfg->sample_rank < 0 || cfg->sample_rank >= (cfg->sample_world > 0 ? cfg->sample_world : 1)) {
     g_create_err = "pt_create: invalid config";
@@ -445,7 +454,8 @@ static SceneView sceneView(const pt_ctx* ctx) {
 
 // make sure the overflow stack covers `threads` threads of a kernel keeping `ldsDepth` entries in LDS
 static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDepth = LDS_STACK) {
-  *ovfDepth = ctx->maxStack > ldsDepth ? ctx->maxStack - ldsDepth + 1 : 0;
+  // pt_trace.h StackT: at most maxStack - ldsDepth/2 - 1 entries are ever in HBM
+  *ovfDepth = ctx->maxStack > ldsDepth ? ctx->maxStack - ldsDepth / 2 : 0;
   if (*ovfDepth == 0) return PT_OK;
   size_t need = threads * (size_t)(*ovfDepth);
   if (need > ctx->ovfInts) {
@@ -578,6 +588,45 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
   return PT_OK;
 }
 
+// Tile splitting (reorderKernel) pays off when the SIMDs have issue slots to
+// spare (the MIS integrator, latency-bound) and costs when they do not (the
+// Lambert megakernel is VALU-bound: a split item's idle lanes still take issue
+// cycles). Results are identical either way, so the runtime measures: after a
+// restart of the running mean (frameCounter 0, as on every camera move in the
+// reference) frames 1-2 run unsplit and 8-9 split (3-7 let the per-tile split
+// state converge), and the faster policy is kept until the next restart.
+// Returns the split percentage for this frame's reorder (0 = off).
+static int splitPolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered) {
+  if (!PT_SPLIT_AUTO || PT_SPLIT_PCT <= 0) return PT_SPLIT_PCT;
+  if (!ordered) return 0;
+  if (frameCounter == 0) {
+    ctx->probeFrame = 0;
+    ctx->splitOnFrames = ctx->splitOffFrames = 0;
+    ctx->splitOnMs = ctx->splitOffMs = 0.0;
+    ctx->splitDecided = -1;
+    if (ctx->d_cost) (void)hipMemsetAsync(ctx->d_cost + 2 * (size_t)ctx->numItems, 0, (size_t)ctx->numItems * sizeof(int),
+                                          ctx->stream);
+  }
+  if (ctx->splitDecided >= 0) return ctx->splitDecided ? PT_SPLIT_PCT : 0;
+  // the previous frame's time (its launch is the last recorded one)
+  const int f = ctx->probeFrame++;
+  if (ctx->launches > 0 && (f == 2 || f == 3 || f == 9 || f == 10)) {
+    float ms = 0.0f;
+    hipEvent_t b = ctx->evs[2 * (ctx->launches - 1)], e = ctx->evs[2 * (ctx->launches - 1) + 1];
+    if (hipEventSynchronize(e) == hipSuccess && hipEventElapsedTime(&ms, b, e) == hipSuccess) {
+      if (f <= 3) { ctx->splitOffMs += ms; ctx->splitOffFrames++; }
+      else { ctx->splitOnMs += ms; ctx->splitOnFrames++; }
+    }
+  }
+  if (f >= 10) {
+    const bool on = ctx->splitOnFrames > 0 && ctx->splitOffFrames > 0 &&
+                    ctx->splitOnMs / ctx->splitOnFrames < ctx->splitOffMs / ctx->splitOffFrames;
+    ctx->splitDecided = on ? 1 : 0;
+    return on ? PT_SPLIT_PCT : 0;
+  }
+  return f >= 3 ? PT_SPLIT_PCT : 0;
+}
+
 int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
@@ -653,19 +702,53 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   // longest-tiles-first: each band's tiles in the order of the previous frame's cost
   const int group = std::max(1, PT_TILE_GROUP);
   const bool ordered = !regen && !count && !(c.flags & PT_FLAG_NO_TILE_ORDER) &&
-                       (ctx->perQueue + group - 1) / group <= REORDER_MAX;
+                       (ctx->perQueue + group - 1) / group <= REORDER_MAX && ctx->numItems < (1 << 22);
+  const int orderCap = 4 * ctx->perQueue + 64;  // room for the items of split tiles
   if (ordered && !ctx->d_cost) {
-    CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * sizeof(int)));
-    CK(hipMalloc(&ctx->d_order, (size_t)ctx->numItems * sizeof(int)));
+    // per tile: summed item cost, longest item, split state (reorderKernel reads and zeroes the costs)
+    CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * 3 * sizeof(int)));
+    CK(hipMemsetAsync(ctx->d_cost, 0, (size_t)ctx->numItems * 3 * sizeof(int), ctx->stream));
+    // per band: orderCap work items, then the NUM_QUEUES item counts (reorderKernel)
+    CK(hipMalloc(&ctx->d_order, ((size_t)NUM_QUEUES * orderCap + NUM_QUEUES) * sizeof(int)));
     ctx->orderValid = false;
   }
+  const int splitPct = splitPolicy(ctx, frameCounter, ordered);
   p.tileOrder = ordered && ctx->orderValid ? ctx->d_order : nullptr;
+  p.orderCap = orderCap;
   p.tileCost = ordered ? ctx->d_cost : nullptr;
+  p.tileCostMax = ordered ? ctx->d_cost + ctx->numItems : nullptr;
+#if PT_WAVE_TRACE
+  // diagnostics build: each wave's {start, end, tiles | longest tile's pixel << 32,
+  // longest tile's duration, its most node-loop / leaf-loop iterations of a lane} (100 MHz wall
+  // clock), appended per frame to $PT_WAVE_TRACE_FILE (tools/wave_trace.py)
+  const size_t nTrace = (size_t)grid * (BLOCK / 64) * 6;
+  unsigned long long* dTrace = nullptr;
+  if (!regen) {
+    CK(hipMalloc(&dTrace, nTrace * sizeof(unsigned long long)));
+    CK(hipMemsetAsync(dTrace, 0, nTrace * sizeof(unsigned long long), ctx->stream));
+  }
+  p.waveTrace = dTrace;
+#endif
   CK(hipEventRecord(evb, ctx->stream));
   if (regen) CK(launchRegen(p, c.integrator, grid, ctx->stream, cull));
   else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
+#if PT_WAVE_TRACE
+  if (dTrace) {
+    std::vector<unsigned long long> tr(nTrace);
+    CK(hipMemcpyAsync(tr.data(), dTrace, nTrace * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(dTrace);
+    if (const char* fn = std::getenv("PT_WAVE_TRACE_FILE")) {
+      if (FILE* f = std::fopen(fn, "ab")) {
+        std::fwrite(tr.data(), sizeof(unsigned long long), nTrace, f);
+        std::fclose(f);
+      }
+    }
+  }
+#endif
   if (ordered) {
-    CK(launchReorder(ctx->d_cost, ctx->d_order, ctx->perQueue, ctx->numItems, group, ctx->stream));
+    CK(launchReorder(ctx->d_cost, ctx->d_cost + ctx->numItems, ctx->d_cost + 2 * (size_t)ctx->numItems, ctx->d_order,
+                     ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, ctx->stream));
     ctx->orderValid = true;
   }
   CK(hipEventRecord(eve, ctx->stream));

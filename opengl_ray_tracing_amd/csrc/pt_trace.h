@@ -15,28 +15,40 @@ struct Counters {
 };
 
 // ----------------------------------------------------------------- stack
-// LDS stack of LDS_STACK entries per lane, entry e of thread t at
-// lds[(e % LDS_STACK) * BLOCK + t]; entries older than the newest LDS_STACK
-// live in the thread's HBM overflow region gbl[e] (only when the tree is
-// deeper than LDS_STACK).
+// LDS stack of up to DEPTH entries per lane, entry e of thread t at
+// lds[(e % DEPTH) * STRIDE + t] (lane-interleaved: a wave's push/pop is bank
+// conflict free). Entries [0, base) live in the thread's HBM overflow region
+// gbl[] (only trees deeper than DEPTH get there): a push onto a full LDS part
+// moves its older half to HBM, and a pop from an empty LDS part brings back up
+// to half a stack at once -- one memory round trip per DEPTH/2 pops. (Moving
+// one entry per push/pop past the LDS depth stalled every deep pop on an L2
+// round trip: the rays that walk deep into a chain-shaped reference-SAH tree
+// made single 8x8 tiles last most of a c4 frame.)
 template <int DEPTH, int STRIDE>
 struct StackT {
   static_assert((DEPTH & (DEPTH - 1)) == 0, "LDS stack depth must be a power of two");
+  static constexpr int HALF = DEPTH / 2;
   int* lds;   // &s_stack[threadIdx.x]
   int* gbl;   // overflow region (may be null when maxStack <= DEPTH)
-  int sp;
+  int sp;     // entries on the stack
+  int base;   // entries in gbl
+  __device__ __forceinline__ void reset() { sp = 0; base = 0; }
   __device__ __forceinline__ void push(int v) {
-    int slot = sp & (DEPTH - 1);
-    if (sp >= DEPTH) gbl[sp - DEPTH] = lds[slot * STRIDE];
-    lds[slot * STRIDE] = v;
+    if (sp - base == DEPTH) {
+      for (int i = 0; i < HALF; i++) gbl[base + i] = lds[((base + i) & (DEPTH - 1)) * STRIDE];
+      base += HALF;
+    }
+    lds[(sp & (DEPTH - 1)) * STRIDE] = v;
     sp++;
   }
   __device__ __forceinline__ int pop() {
+    if (sp == base) {
+      const int n = base < HALF ? base : HALF;
+      base -= n;
+      for (int i = 0; i < n; i++) lds[((base + i) & (DEPTH - 1)) * STRIDE] = gbl[base + i];
+    }
     sp--;
-    int slot = sp & (DEPTH - 1);
-    int v = lds[slot * STRIDE];
-    if (sp >= DEPTH) lds[slot * STRIDE] = gbl[sp - DEPTH];
-    return v;
+    return lds[(sp & (DEPTH - 1)) * STRIDE];
   }
 };
 using Stack = StackT<LDS_STACK, BLOCK>;
@@ -149,11 +161,15 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
   int best = -1;
   int ref = S.rootRef;   // next item in visiting order (REF_NONE only when the stack is empty too)
   int leaf = REF_NONE;   // parked leaf, precedes ref
-  st.sp = 0;
+  st.reset();
   C.rays++;
   while (true) {
     // node phase
     while (ref >= 0) {
+      if (PT_WAVE_TRACE && !COUNT) {  // diagnostics build: node-loop iterations (lane, wave)
+        C.nodes++;
+        if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
+      }
       NodeHit nh;
       const float4* nd = S.bvh + 4 * (size_t)ref;
       if (LDSTOP && ref < S.nTop) nd = top + 4 * ref;
@@ -222,6 +238,10 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
       if (false)
 #endif
       for (int k = 0; k < cnt; k += 2) {
+        if (PT_WAVE_TRACE && !COUNT) {  // diagnostics build: leaf-loop iterations (lane, wave)
+          C.tris++;
+          if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
+        }
         const int i = start + k;
         const float4* g = S.geo + 4 * (size_t)i;
         const float4 A0 = g[0], B0 = g[1], C0 = g[2], N0 = g[3];
@@ -266,20 +286,33 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
 // round-robin. One tile per atomic measured best:
 // claiming 2 or 4 per atomic, interleaving the queues or grouping an XCD's
 // queues into one band were all slower or neutral.
-// order (may be null = identity) permutes the tiles within each queue's band:
-// the megakernel hands out each band's most expensive tiles of the previous
-// frame first (renderKernel / reorderKernel), so long paths start early instead
-// of forming the frame's tail.
+// order (may be null = identity) replaces each queue's band by a list of work
+// items built from the previous frame (reorderKernel): a tile whose paths form
+// the frame's tail runs as 2^lg items of 64 >> lg pixels each (lg adapted per
+// tile from frame to frame), longest items first, so the longest paths of a
+// frame run side by side on otherwise idle SIMDs instead of forming its tail.
+// Item encoding: tile | sub << 22 | lg << 28 (pixels [sub*(64>>lg), (sub+1)*(64>>lg))
+// of the tile, row-major); order[q * orderCap + i], i < order[NUM_QUEUES * orderCap + q].
+constexpr int ITEM_TILE_BITS = 22;
+constexpr int MAX_SPLIT_LG = 6;
+__device__ __forceinline__ int itemTile(int item) { return item & ((1 << ITEM_TILE_BITS) - 1); }
+__device__ __forceinline__ int itemSub(int item) { return (item >> ITEM_TILE_BITS) & 63; }
+__device__ __forceinline__ int itemLg(int item) { return (item >> 28) & 7; }
 struct TileCursor {
   int qi = 0;  // queues found empty (wave-uniform)
-  __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home, const int* order) {
+  __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home, const int* order = nullptr,
+                                      int orderCap = 0) {
     while (qi < NUM_QUEUES) {
       const int q = (home + qi) & (NUM_QUEUES - 1);
       int it = 0;
       if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
       it = __shfl(it, 0, 64);
-      const int t = q * perQueue + it;
-      if (it < perQueue && t < numItems) return order ? order[t] : t;
+      if (order) {
+        if (it < order[NUM_QUEUES * orderCap + q]) return order[q * orderCap + it];
+      } else {
+        const int t = q * perQueue + it;
+        if (it < perQueue && t < numItems) return t;
+      }
       qi++;
     }
     return -1;

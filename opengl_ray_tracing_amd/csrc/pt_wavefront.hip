@@ -58,9 +58,9 @@ __device__ __forceinline__ bool ownedPixel(const WFParams& p, int k, int& px, in
 
 __device__ __forceinline__ void finishPixel(const WFParams& p, int pid, V3 color) {
   float4* a = p.accum + pid;
-  float4 old = *a;
+  float4 old = ldStream(a);
   float w = 1.0f / (float)(p.frameCounter + 1u);
-  *a = make_float4(mixf(old.x, color.x, w), mixf(old.y, color.y, w), mixf(old.z, color.z, w), 1.0f);
+  stStream(a, make_float4(mixf(old.x, color.x, w), mixf(old.y, color.y, w), mixf(old.z, color.z, w), 1.0f));
 }
 
 // -------------------------------------------------------------- gen: main() IS:846-850
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(BLOCK) void wfTraceKernel(WFTraceParams p) {
   st.lds = s_stack + threadIdx.x;
   const size_t gtid = (size_t)blockIdx.x * BLOCK + threadIdx.x;
   st.gbl = p.ovf ? p.ovf + gtid * p.ovfDepth : nullptr;
-  st.sp = 0;
+  st.reset();
   const int seg = blockIdx.x & (WF_NSEG - 1);
   const int n = p.count[seg * CTL_LINE_INTS];
   const int* q = p.queue + (size_t)seg * p.segCap;
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(BLOCK) void wfTraceKernel(WFTraceParams p) {
       inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
       tbest = PT_INF;
       best = -1;
-      st.sp = 0;
+      st.reset();
       ref = S.rootRef;
       leafI = leafEnd = 0;
       if (ref < 0 && ref != REF_NONE) {

@@ -14,9 +14,11 @@ PASSES=(
   "B:SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VMEM"
   "C:TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum"
   "D:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_VMEM SQ_LEVEL_WAVES SQ_INSTS_SMEM SQ_WAVES_LT_64 SQ_INSTS_VSKIPPED SQ_ACTIVE_INST_SCA"
+  "E:TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum"
 )
 for p in "${PASSES[@]}"; do
   name="${p%%:*}"; ctr="${p#*:}"
+  [ -n "$ONLY" ] && [[ "$ONLY" != *"$name"* ]] && continue   # ONLY=AE: a subset of the passes
   timeout -k 10 300 rocprofv3 --pmc $ctr -f csv -d "$OUT/$name" -o run -- "${RUN[@]}" > "$OUT/$name.log" 2>&1; rc=$?
   echo "pass $name=$rc"; [ $rc -eq 0 ] || exit $rc
 done

@@ -40,6 +40,8 @@ def main():
         print(f"   L2 hit                    {g('TCC_HIT_sum') / (g('TCC_HIT_sum') + g('TCC_MISS_sum')):.3f}")
         print(f"   VALU insts per wave       {g('SQ_INSTS_VALU') / g('SQ_WAVES'):.0f}")
         print(f"   VMEM rd per wave          {g('SQ_INSTS_VMEM_RD') / g('SQ_WAVES'):.0f}")
+        print(f"   TA busy / GPU busy        {g('TA_BUSY_avr') / g('GRBM_GUI_ACTIVE'):.3f}")
+        print(f"   L1 (TCP) hit              {1 - g('TCP_TCC_READ_REQ_sum') / g('TCP_TOTAL_CACHE_ACCESSES_sum'):.3f}")
 
 
 if __name__ == "__main__":

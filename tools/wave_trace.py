@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarise the megakernel wave lifetimes of a PT_WAVE_TRACE=1 build.
+
+    python tools/tune.py --build wtrace:PT_WAVE_TRACE=1            # here
+    PT_WAVE_TRACE_FILE=gpurun_out/w.bin python tools/tune.py --child wtrace --config c4 --frames 3 --warmup 0
+    python tools/wave_trace.py gpurun_out/w.bin
+
+Per frame: how long the frame lasted (first wave start to last wave end), how
+much of it the average wave was alive, the frame's tail (time from the median
+wave end to the last), and the longest single tile.
+"""
+import sys
+
+import numpy as np
+
+
+def main():
+    raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 6)
+    at = (raw[:, 2] >> np.uint64(32)).astype(np.int64)  # (px << 16 | py) of the wave's longest tile
+    raw[:, 2] &= np.uint64(0xffffffff)
+    wit = (raw[:, 5] >> np.uint64(32)).astype(np.int64)  # the wave's own loop iterations in that tile
+    raw[:, 5] &= np.uint64(0xffffffff)
+    a = raw.astype(np.float64)
+    # frames are appended one after another; a frame's records start where the start clock jumps back
+    n = len(a)
+    starts = a[:, 0]
+    valid = starts > 0
+    # split into frames by equal sizes (every frame uses the same grid)
+    per = int(sys.argv[2]) if len(sys.argv) > 2 else None
+    if per is None:
+        for cand in range(1, n + 1):
+            if n % cand == 0 and cand >= 256 and np.all(np.diff(starts[:cand][valid[:cand]]) < 1e7):
+                per = cand
+        per = per or n
+    for f in range(n // per):
+        r = a[f * per:(f + 1) * per]
+        rat = at[f * per:(f + 1) * per][r[:, 0] > 0]
+        rwit = wit[f * per:(f + 1) * per][r[:, 0] > 0]
+        r = r[r[:, 0] > 0]
+        t0, t1 = r[:, 0].min(), r[:, 1].max()
+        life = (r[:, 1] - r[:, 0]).mean()
+        ends = np.sort(r[:, 1])
+        us = lambda x: x / 100.0  # 100 MHz ticks -> us
+        print(f"frame {f}: {len(r)} waves, frame {us(t1 - t0):8.1f} us, mean wave life {us(life):8.1f} us "
+              f"({life / (t1 - t0):.2f}), start spread {us(r[:, 0].max() - t0):6.1f} us, "
+              f"tail (median end -> last end) {us(t1 - np.median(ends)):7.1f} us, "
+              f"last 1% of waves {us(t1 - ends[int(0.99 * len(ends))]):6.1f} us, "
+              f"tiles/wave {r[:, 2].mean():.1f}, longest tile {us(r[:, 3].max()):7.1f} us")
+        top = np.argsort(-r[:, 3])[:5]
+        print("   longest tiles (px, py of the tile corner: us, most node / leaf iterations of a lane,"
+              " the wave's loop iterations):",
+              ", ".join(f"({rat[k] >> 16}, {rat[k] & 0xffff}): {us(r[k, 3]):.0f} us {r[k, 4]:.0f}/{r[k, 5]:.0f}"
+                        f" wave {rwit[k]}" for k in top))
+
+
+if __name__ == "__main__":
+    main()
