@@ -80,6 +80,8 @@ typedef struct pt_frame_stats {
   float kernel_ms_total;/* summed device time of the render launches since the reset */
   int launches;         /* render launches since the reset */
   int max_stack;        /* traversal stack bound used (tree depth + 1) */
+  int split_items;      /* megakernel: work items the next frame's schedule adds by splitting
+                           long-path tiles (0 = one item per tile) */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;

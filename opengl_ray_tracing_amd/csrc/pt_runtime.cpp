@@ -62,7 +62,7 @@ struct pt_ctx {
   int probeFrame = 0, splitOnFrames = 0, splitOffFrames = 0;
   double splitOnMs = 0.0, splitOffMs = 0.0;
   int splitDecided = -1;   // -1 probing, 0 off, 1 on
-  int lastSplit = 0;       // the policy of the last reorder launch
+  int orderCap = 0;        // work items per band in d_order
   bool orderValid = false;
   size_t ovfInts = 0;
   // shards
@@ -704,6 +704,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   const bool ordered = !regen && !count && !(c.flags & PT_FLAG_NO_TILE_ORDER) &&
                        (ctx->perQueue + group - 1) / group <= REORDER_MAX && ctx->numItems < (1 << 22);
   const int orderCap = 4 * ctx->perQueue + 64;  // room for the items of split tiles
+  ctx->orderCap = orderCap;
   if (ordered && !ctx->d_cost) {
     // per tile: summed item cost, longest item, split state (reorderKernel reads and zeroes the costs)
     CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * 3 * sizeof(int)));
@@ -914,6 +915,14 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   }
   st->launches = ctx->launches;
   st->max_stack = ctx->maxStack;
+  st->split_items = 0;
+  if (ctx->d_order && ctx->orderValid) {
+    int counts[NUM_QUEUES];
+    CK(hipMemcpy(counts, ctx->d_order + (size_t)NUM_QUEUES * ctx->orderCap, sizeof(counts), hipMemcpyDeviceToHost));
+    long items = 0;
+    for (int q = 0; q < NUM_QUEUES; q++) items += counts[q];
+    st->split_items = (int)std::max(0L, items - (long)ctx->numItems);
+  }
   return PT_OK;
 }
 

@@ -44,6 +44,7 @@ class FrameStats:
     kernel_ms_total: float
     launches: int
     max_stack: int
+    split_items: int
 
 
 def _fp(a: np.ndarray):
@@ -192,7 +193,7 @@ class Renderer:
         s = _native.PtFrameStats()
         self._ck(self._lib.pt_get_stats(self._h, C.byref(s)), "pt_get_stats")
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
-                          s.kernel_ms_total, s.launches, s.max_stack)
+                          s.kernel_ms_total, s.launches, s.max_stack, s.split_items)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

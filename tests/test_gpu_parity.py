@@ -129,6 +129,27 @@ def test_frame_kernels_agree(request, name, integrator):
         assert sa.rays == sb.rays == sc.rays
 
 
+def test_tile_splitting_does_not_change_the_image(c4):
+    """Long-path tiles split into smaller work items (frames 4-10 after a restart, while the
+    runtime probes the split policy) only regroup lanes: the image equals the fixed-order,
+    one-item-per-tile one bit for bit, with the same rays, and splitting did happen."""
+    from opengl_ray_tracing_amd import FLAG_NO_TILE_ORDER
+    cfg, tris, nodes, hdr = c4
+    eye, rot = orbit_camera(*cfg.camera)
+    split_seen = 0
+    with Renderer(W, H, cfg.integrator, max_bounce=cfg.max_bounce) as r:
+        r.upload_scene(tris, nodes)
+        r.upload_env(hdr)
+        for f in range(12):
+            r.render_frame(eye, rot, f)
+            split_seen = max(split_seen, r.stats().split_items)
+        a, sa = r.accum(), r.stats()
+    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=12, flags=FLAG_NO_TILE_ORDER)
+    assert split_seen > 0
+    assert np.array_equal(a, b)
+    assert sa.rays == sb.rays
+
+
 def test_tile_order_does_not_change_the_image(c4):
     """Longest-tiles-first scheduling (default) only reorders work: frames after the first use the
     previous frame's per-tile costs, and the image equals the fixed-order one bit for bit."""
