@@ -47,6 +47,7 @@ constexpr size_t CTL_QUEUES = 0;                                      // NUM_QUE
 constexpr size_t CTL_STATS = 64 * 256;                                // 5 u64 cumulative fetch counters
 constexpr size_t CTL_RAYS = 65 * 256;                                 // RAY_SHARDS padded u64 counters
 constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
+constexpr int PAIR_F4 = 7;        // float4 per pair record (26 floats: p1, p2, p3, Ng, w of two triangles)
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;
 constexpr int MAX_LEAF = 1 << LEAF_CNT_BITS;
@@ -55,6 +56,7 @@ constexpr int MAX_TRIS = (1 << (31 - LEAF_CNT_BITS)) - 1;
 // Device-resident scene (relaid out at upload, see pt_runtime.cpp)
 struct SceneView {
   const float4* geo;   // 4 float4 per triangle: (p1, w=dot(Ng,p1)), (p2, 0), (p3, 0), (Ng, 0)
+  const float4* pairs; // PAIR_F4 float4 per triangle i: triangles i and i+1 component-interleaved (pt_trace.h pairTest)
   const float* attr;   // 36 f32 per triangle: the Triangle_encoded record (normals, material)
   const float4* bvh;   // 4 float4 per device node id (pt_runtime.cpp: top of the tree first, breadth-first)
   int nTop;            // device ids [0, nTop) are the top of the tree, staged in LDS by the megakernel

@@ -37,6 +37,7 @@ struct pt_ctx {
   int numCU = 0;
   // scene
   float4* d_geo = nullptr;
+  float4* d_pairs = nullptr;  // triangles i and i+1 component-interleaved (SceneView::pairs)
   float* d_attr = nullptr;
   float4* d_bvh = nullptr;
   int nDevNodes = 0;  // internal nodes in d_bvh (device ids 0..nDevNodes-1)
@@ -186,7 +187,7 @@ void pt_destroy(pt_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->cfg.device_id);
   if (ctx->own) (void)hipStreamSynchronize(ctx->own);
-  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh);
+  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
@@ -308,7 +309,23 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
   }
   int rootRef = encodeRef(1);
   if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
-  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh);
+  // pair records: triangle i (x) and i + 1 (y, zeros past the last), PAIR_F4 float4 each
+  std::vector<float4> pairs((size_t)nTri * PAIR_F4, make_float4(0, 0, 0, 0));
+  for (int i = 0; i < nTri; i++) {
+    const float4* A = &geo[4 * (size_t)i];
+    const float4* B = &geo[4 * (size_t)(i + 1)];  // the zero record past the last triangle
+    float4* r = &pairs[(size_t)i * PAIR_F4];
+    r[0] = make_float4(A[0].x, B[0].x, A[0].y, B[0].y);  // p1.x, p1.y
+    r[1] = make_float4(A[0].z, B[0].z, A[1].x, B[1].x);  // p1.z, p2.x
+    r[2] = make_float4(A[1].y, B[1].y, A[1].z, B[1].z);  // p2.y, p2.z
+    r[3] = make_float4(A[2].x, B[2].x, A[2].y, B[2].y);  // p3.x, p3.y
+    r[4] = make_float4(A[2].z, B[2].z, A[3].x, B[3].x);  // p3.z, Ng.x
+    r[5] = make_float4(A[3].y, B[3].y, A[3].z, B[3].z);  // Ng.y, Ng.z
+    r[6] = make_float4(A[0].w, B[0].w, 0.0f, 0.0f);      // w = dot(Ng, p1)
+  }
+  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
+  CK(hipMalloc(&ctx->d_pairs, pairs.size() * sizeof(float4)));
+  CK(hipMemcpy(ctx->d_pairs, pairs.data(), pairs.size() * sizeof(float4), hipMemcpyHostToDevice));
   CK(hipMalloc(&ctx->d_geo, geo.size() * sizeof(float4)));
   CK(hipMalloc(&ctx->d_attr, (size_t)nTri * 36 * sizeof(float)));
   CK(hipMalloc(&ctx->d_bvh, bvh.size() * sizeof(float4)));
@@ -444,6 +461,7 @@ static uint32_t sampleIndex(const pt_config& c, uint32_t frameCounter) {
 static SceneView sceneView(const pt_ctx* ctx) {
   SceneView s;
   s.geo = ctx->d_geo;
+  s.pairs = ctx->d_pairs;
   s.attr = ctx->d_attr;
   s.bvh = ctx->d_bvh;
   s.nTop = std::min(LDS_NODES, ctx->nDevNodes);

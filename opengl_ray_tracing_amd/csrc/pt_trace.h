@@ -79,13 +79,6 @@ struct NodeHit {
 };
 __device__ __forceinline__ void visitNode(const float4* nd, V3 o, V3 inv, NodeHit& h) {
   const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-#ifdef PT_SCALAR_SLAB
-  h.d1 = hitAABB(o, inv, make_float4(q0.x, q0.z, q1.x, 0), make_float4(q1.z, q2.x, q2.z, 0), h.t0l);
-  h.d2 = hitAABB(o, inv, make_float4(q0.y, q0.w, q1.y, 0), make_float4(q1.w, q2.y, q2.w, 0), h.t0r);
-  h.lref = __float_as_int(q3.x);
-  h.rref = __float_as_int(q3.y);
-  return;
-#endif
   const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
   const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
   const f32x2 lox = {q0.x, q0.y}, loy = {q0.z, q0.w}, loz = {q1.x, q1.y};
@@ -128,6 +121,42 @@ __device__ __forceinline__ bool triTest(float4 A, float4 B, float4 C, float4 Nn,
   t = tt;
   return !(fabsf(dn) < 0.00001f) && !(tt < 0.0005f) && (tt < tmax) && (r1 || r2);
 }
+// triTest of triangles i and i+1 at once from their pair record (pt_runtime.cpp):
+// every operation of triTest on float2 pairs (x = triangle i, y = i+1), so the
+// packed adds and multiplies (v_pk_add_f32 / v_pk_mul_f32) round exactly like
+// the scalar ones and each pair costs about half the VALU of two triTests.
+// g0/g1: accepted apart from the caller's closest-hit bound.
+__device__ __forceinline__ void pairTest(const float4* r, V3 o, V3 d, float& t0, float& t1, bool& g0, bool& g1) {
+  const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6];
+  const f32x2 p1x = {q0.x, q0.y}, p1y = {q0.z, q0.w}, p1z = {q1.x, q1.y};
+  const f32x2 p2x = {q1.z, q1.w}, p2y = {q2.x, q2.y}, p2z = {q2.z, q2.w};
+  const f32x2 p3x = {q3.x, q3.y}, p3y = {q3.z, q3.w}, p3z = {q4.x, q4.y};
+  const f32x2 nx = {q4.z, q4.w}, ny = {q5.x, q5.y}, nz = {q5.z, q5.w};
+  const f32x2 w = {q6.x, q6.y};
+  const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+  const f32x2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+  const f32x2 dn = (nx * dx + ny * dy) + nz * dz;           // dot(N, d)
+  const f32x2 num = w - ((ox * nx + oy * ny) + oz * nz);    // A.w - dot(o, N)
+  const f32x2 tt = {num.x / dn.x, num.y / dn.y};
+  const f32x2 Px = ox + dx * tt, Py = oy + dy * tt, Pz = oz + dz * tt;
+  // dot(cross(b - a, P - a), N)
+  auto edge = [&](f32x2 ax, f32x2 ay, f32x2 az, f32x2 bx, f32x2 by, f32x2 bz) -> f32x2 {
+    const f32x2 ex = bx - ax, ey = by - ay, ez = bz - az;
+    const f32x2 vx = Px - ax, vy = Py - ay, vz = Pz - az;
+    const f32x2 cx = ey * vz - vy * ez, cy = ez * vx - vz * ex, cz = ex * vy - vx * ey;
+    return (cx * nx + cy * ny) + cz * nz;
+  };
+  const f32x2 s1 = edge(p1x, p1y, p1z, p2x, p2y, p2z);
+  const f32x2 s2 = edge(p2x, p2y, p2z, p3x, p3y, p3z);
+  const f32x2 s3 = edge(p3x, p3y, p3z, p1x, p1y, p1z);
+  t0 = tt.x;
+  t1 = tt.y;
+  g0 = !(fabsf(dn.x) < 0.00001f) && !(tt.x < 0.0005f) &&
+       ((s1.x > 0 && s2.x > 0 && s3.x > 0) || (s1.x < 0 && s2.x < 0 && s3.x < 0));
+  g1 = !(fabsf(dn.y) < 0.00001f) && !(tt.y < 0.0005f) &&
+       ((s1.y > 0 && s2.y > 0 && s3.y > 0) || (s1.y < 0 && s2.y < 0 && s3.y < 0));
+}
+
 __device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, float& t) {
   return triTest(g[0], g[1], g[2], g[3], o, d, tmax, t);
 }
@@ -216,55 +245,34 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
       leaf = REF_NONE;
       if (COUNT) C.nodes++;
       float localBest = PT_INF;
-      // two triangles per iteration, their eight records fetched together (one
-      // memory round trip per pair; the geometry buffer carries one zero record
-      // past the last triangle); tested in index order with the running tbest
-#ifdef PT_TRI_SINGLE
-      for (int k = 0; k < cnt; k++) {
-        const int i = start + k;
-        const float4* g = S.geo + 4 * (size_t)i;
-        float t0;
-        if (COUNT) {
-          bool h0 = triTest(g[0], g[1], g[2], g[3], o, d, PT_INF, t0);
-          C.tris++;
-          if (h0 && t0 < localBest) { localBest = t0; C.mats++; }
-          if (h0 && t0 < tbest) { tbest = t0; best = i; }
-        } else if (triTest(g[0], g[1], g[2], g[3], o, d, tbest, t0)) {
-          tbest = t0;
-          best = i;
-          if (ANYHIT || anyRT) { tOut = tbest; return best; }
-        }
-      }
-      if (false)
-#endif
+      // two triangles per iteration from one pair record (one memory round trip,
+      // packed math: pairTest; the last record pairs with zeros), accepted in
+      // index order against the running tbest
       for (int k = 0; k < cnt; k += 2) {
         if (PT_WAVE_TRACE && !COUNT) {  // diagnostics build: leaf-loop iterations (lane, wave)
           C.tris++;
           if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
         }
         const int i = start + k;
-        const float4* g = S.geo + 4 * (size_t)i;
-        const float4 A0 = g[0], B0 = g[1], C0 = g[2], N0 = g[3];
-        const float4 A1 = g[4], B1 = g[5], C1 = g[6], N1 = g[7];
         const bool second = k + 1 < cnt;
         float t0, t1;
+        bool g0, g1;
+        pairTest(S.pairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1);
         if (COUNT) {
-          bool h0 = triTest(A0, B0, C0, N0, o, d, PT_INF, t0);
-          bool h1 = triTest(A1, B1, C1, N1, o, d, PT_INF, t1) & second;
+          const bool h0 = g0 && t0 < PT_INF;
+          const bool h1 = g1 && t1 < PT_INF && second;
           C.tris += 1u + (second ? 1u : 0u);
           if (h0 && t0 < localBest) { localBest = t0; C.mats++; }
           if (h0 && t0 < tbest) { tbest = t0; best = i; }
           if (h1 && t1 < localBest) { localBest = t1; C.mats++; }
           if (h1 && t1 < tbest) { tbest = t1; best = i + 1; }
         } else {
-          const bool h0 = triTest(A0, B0, C0, N0, o, d, tbest, t0);
-          if (h0) {
+          if (g0 && t0 < tbest) {
             tbest = t0;
             best = i;
             if (ANYHIT || anyRT) { tOut = tbest; return best; }
           }
-          const bool h1 = triTest(A1, B1, C1, N1, o, d, tbest, t1) & second;
-          if (h1) {
+          if (g1 && second && t1 < tbest) {
             tbest = t1;
             best = i + 1;
             if (ANYHIT || anyRT) { tOut = tbest; return best; }
