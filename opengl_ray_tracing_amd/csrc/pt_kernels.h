@@ -47,6 +47,10 @@ constexpr size_t CTL_QUEUES = 0;                                      // NUM_QUE
 constexpr size_t CTL_STATS = 64 * 256;                                // 5 u64 cumulative fetch counters
 constexpr size_t CTL_RAYS = 65 * 256;                                 // RAY_SHARDS padded u64 counters
 constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
+#ifndef PT_PACKETS
+#define PT_PACKETS 1  // megakernel: camera rays as wave packets (pt_trace.h tracePacket)
+#endif
+constexpr int PKT_DEPTH = 128;    // camera-ray packet stack entries per wave (LDS); deeper trees trace per ray
 constexpr int PAIR_F4 = 7;        // float4 per pair record (26 floats: p1, p2, p3, Ng, w of two triangles)
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;
@@ -92,6 +96,7 @@ struct RenderParams {
   int rank, world;
   int* ovf;             // traversal stack overflow (per thread ovfDepth ints), may be null
   int ovfDepth;
+  int packets;          // camera rays traced as wave packets (tree depth fits PKT_DEPTH)
   unsigned long long* stats;  // [rays, nodes, tris, mats, texels]
   unsigned long long* rayShards;  // RAY_SHARDS ray counters (stride RAY_SHARD_STRIDE)
   const int* tileOrder; // per-band work items (null = one per tile, in id order), then NUM_QUEUES item

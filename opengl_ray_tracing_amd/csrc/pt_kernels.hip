@@ -218,6 +218,28 @@ __device__ __forceinline__ int primaryPixel(const RenderParams& p, int px, int p
   return tri;
 }
 
+// primaryPixel for a whole wave: the camera rays of the wave's pixels traced as
+// one packet (tracePacket); a ray that met an exact tie is retraced in the
+// reference order. All 64 lanes call it; valid marks the lanes with a pixel.
+template <bool CULL>
+__device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int py, bool valid, Stack& st, Counters& C,
+                                             const float4* top, PacketEntry* pstack, float& t) {
+  uint32_t seed;
+  const V3 dir = cameraRay(p, valid ? px : 0, valid ? py : 0, seed);
+  const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+  bool tie;
+  int tri = tracePacket<CULL>(p.scene, eye, dir, valid, t, tie, pstack, C, top);
+  if (valid && tie) {
+    C.rays--;  // the same ray, counted once
+    tri = traceRay<false, CULL, false, Stack, (LDS_NODES > 0)>(p.scene, eye, dir, t, st, C, false, top);
+  }
+  if (valid && tri < 0) {
+    const V3 color = sampleHdr(p.env, dir);
+    accumulate(p, px, py, color, C, false);
+  }
+  return tri;
+}
+
 // the rest of the path of a pixel whose camera ray hit triangle tri at t
 template <int INTEG, bool CULL, bool COUNT>
 __device__ __forceinline__ void finishPixel(const RenderParams& p, int px, int py, int tri, float t, Stack& st,
@@ -530,6 +552,8 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
   Counters C = {0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   const int home = blockIdx.x & (NUM_QUEUES - 1);
+  __shared__ PacketEntry s_packet[BLOCK / 64][COUNT ? 1 : PKT_DEPTH];  // camera-ray packet stacks
+  PacketEntry* pstack = s_packet[threadIdx.x >> 6];
   const int tilesPerShard = p.shardTiles;  // 8x8 wave tiles per shard tile
   const int sub = p.shardSize >> 3;        // wave tiles per shard-tile edge
 #if PT_WAVE_TRACE
@@ -559,7 +583,12 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
     const int k = itemSub(item) * nLanes + lane;
     const int px = gx * p.shardSize + (s % sub) * 8 + (k & 7);
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
-    if (lane < nLanes && px < p.width && py < p.height) {
+    const bool valid = lane < nLanes && px < p.width && py < p.height;
+    if (!COUNT && p.packets) {
+      float t;
+      const int tri = primaryPacket<CULL>(p, px, py, valid, st, C, top, pstack, t);
+      if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);
+    } else if (valid) {
       float t;
       const int tri = primaryPixel<CULL, COUNT>(p, px, py, st, C, top, t);
       if (tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);

@@ -715,6 +715,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   p.world = c.tile_world;
   p.ovf = ovfDepth ? ctx->d_ovf : nullptr;
   p.ovfDepth = ovfDepth;
+  p.packets = PT_PACKETS && ctx->maxStack <= PKT_DEPTH;
   p.stats = stats;
   p.rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAYS);
   // longest-tiles-first: each band's tiles in the order of the previous frame's cost

@@ -285,6 +285,101 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
   return best;
 }
 
+// ----------------------------------------------------------------- camera-ray packets
+// Closest hit of a wave's 64 camera rays as one packet (the rays of an 8x8 tile
+// share the eye and nearly their direction, so they walk nearly the same
+// nodes): the wave walks the tree once, each node record is a wave-uniform
+// (scalar) load, every lane tests its own ray against both children's boxes
+// with hitAABB, and a child is entered with the mask of the lanes whose own
+// test hit it -- so each ray intersects exactly the leaves the reference
+// traversal of that ray reaches (minus the ones culled by its current closest
+// hit), only in a different order. Order only matters for exact ties (two
+// triangles at the same t): a lane that meets a triangle at exactly its current
+// closest t reports tie = true, and the caller retraces that ray with traceRay
+// (the reference order). Children are entered nearer-first by majority vote of
+// the lanes that hit both. pstack: this wave's LDS stack of (node, mask),
+// PKT_DEPTH deep (the host enables packets only for trees that fit).
+struct PacketEntry {
+  int ref;
+  int pad;
+  unsigned long long mask;
+};
+template <bool CULL>
+__device__ __forceinline__ int tracePacket(const SceneView& S, V3 o, V3 d, bool valid, float& tOut, bool& tie,
+                                           PacketEntry* pstack, Counters& C, const float4* top) {
+  const int lane = __lane_id();
+  const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  float tbest = PT_INF;
+  int best = -1;
+  tie = false;
+  unsigned long long mask = __ballot(valid);
+  if (valid) C.rays++;
+  int ref = __builtin_amdgcn_readfirstlane(S.rootRef);
+  int sp = 0;
+  while (true) {
+    if (ref >= 0) {  // internal node: one scalar record for the wave
+      NodeHit nh;
+      if (top && ref < S.nTop) visitNode(top + 4 * ref, o, inv, nh);  // LDS broadcast
+      else visitNode(S.bvh + 4 * (size_t)ref, o, inv, nh);
+      nh.lref = __builtin_amdgcn_readfirstlane(nh.lref);
+      nh.rref = __builtin_amdgcn_readfirstlane(nh.rref);
+      const bool active = (mask >> lane) & 1ull;
+      bool h1 = active && nh.lref != REF_NONE && nh.d1 > 0.0f;
+      bool h2 = active && nh.rref != REF_NONE && nh.d2 > 0.0f;
+      if (CULL) {
+        const float lim = tbest + 1e-3f * fmaxf(1.0f, tbest);
+        h1 = h1 && !(nh.t0l > lim);
+        h2 = h2 && !(nh.t0r > lim);
+      }
+      const unsigned long long m1 = __ballot(h1), m2 = __ballot(h2);
+      if (m1 && m2) {
+        const int left = __popcll(__ballot(h1 && h2 && nh.d1 < nh.d2));
+        const int right = __popcll(__ballot(h1 && h2 && !(nh.d1 < nh.d2)));
+        const bool leftFirst = left >= right;
+        if (lane == 0) {
+          pstack[sp].ref = leftFirst ? nh.rref : nh.lref;
+          pstack[sp].mask = leftFirst ? m2 : m1;
+        }
+        sp++;
+        ref = leftFirst ? nh.lref : nh.rref;
+        mask = leftFirst ? m1 : m2;
+        continue;
+      }
+      if (m1 | m2) {
+        ref = m1 ? nh.lref : nh.rref;
+        mask = m1 ? m1 : m2;
+        continue;
+      }
+    } else if (ref != REF_NONE) {  // leaf: its triangle pairs, scalar records
+      const uint32_t v = ~(uint32_t)ref;
+      const int start = (int)(v >> LEAF_CNT_BITS);
+      const int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
+      const bool active = (mask >> lane) & 1ull;
+      for (int k = 0; k < cnt; k += 2) {  // wave-uniform loop: the pair records are scalar loads
+        const int i = start + k;
+        float t0, t1;
+        bool g0, g1;
+        pairTest(S.pairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1);
+        g0 = g0 && active;
+        g1 = g1 && active && k + 1 < cnt;
+        if (g0 && t0 == tbest) tie = true;
+        if (g0 && t0 < tbest) { tbest = t0; best = i; }
+        if (g1 && t1 == tbest) tie = true;
+        if (g1 && t1 < tbest) { tbest = t1; best = i + 1; }
+      }
+    }
+    // pop the next (node, lanes) the packet still has to visit
+    if (sp == 0) break;
+    sp--;
+    ref = __builtin_amdgcn_readfirstlane(pstack[sp].ref);
+    const unsigned long long m = pstack[sp].mask;
+    mask = (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m) |
+           (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32)) << 32;
+  }
+  tOut = tbest;
+  return best;
+}
+
 // ----------------------------------------------------------------- work queue
 // The next 8x8 wave tile for the calling wave (wave-uniform; -1 when every queue is
 // drained). Queue q holds tiles [q*perQueue, (q+1)*perQueue): one contiguous
@@ -302,7 +397,10 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
 // Item encoding: tile | sub << 22 | lg << 28 (pixels [sub*(64>>lg), (sub+1)*(64>>lg))
 // of the tile, row-major); order[q * orderCap + i], i < order[NUM_QUEUES * orderCap + q].
 constexpr int ITEM_TILE_BITS = 22;
-constexpr int MAX_SPLIT_LG = 6;
+#ifndef PT_MAX_SPLIT_LG
+#define PT_MAX_SPLIT_LG 6
+#endif
+constexpr int MAX_SPLIT_LG = PT_MAX_SPLIT_LG;
 __device__ __forceinline__ int itemTile(int item) { return item & ((1 << ITEM_TILE_BITS) - 1); }
 __device__ __forceinline__ int itemSub(int item) { return (item >> ITEM_TILE_BITS) & 63; }
 __device__ __forceinline__ int itemLg(int item) { return (item >> 28) & 7; }
