@@ -39,7 +39,7 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "Mrays/sec + ms/frame (1 spp, 1080p) at 1/2/4/8 MI355X; CPU-ref spp-matched PSNR"
-PROBE_FRAMES = 12  # frames after a restart during which the renderer measures its tile-split policy
+PROBE_FRAMES = 14  # frames after a restart during which the renderer measures its tree and split policies
 
 
 def parse():
@@ -131,8 +131,8 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    # The renderer picks its tile-split policy from measurements on the first 11
-    # frames after a running-mean restart (pt_runtime.cpp splitPolicy); those
+    # The renderer picks its tree and tile-split policies from measurements on the
+    # first 13 frames after a running-mean restart (pt_runtime.cpp probePolicy); those
     # frames run before the W warmup steps, so the timed frames are the
     # progressive steady state (same image, bit for bit, either way).
     for f in range(PROBE_FRAMES):
@@ -196,6 +196,9 @@ def main():
                        "spp_per_frame": 1, "integrator": cfg.integrator, "max_bounce": cfg.max_bounce,
                        "triangles": int(tris.shape[0]), "bvh_nodes": int(nodes.shape[0]),
                        "bvh_builder": args.builder or cfg.builder, "env": cfg.env,
+                       # the tree the timed frames traversed: the uploaded one, or the runtime's own
+                       # binned-SAH tree with every result checked against the uploaded one
+                       "traversal_tree": "runtime (checked against uploaded)" if st.runtime_tree else "uploaded",
                        "parallelism": (f"screen-tile x{n}" + (" + RCCL gather per frame" if n > 1 else ""))
                        if args.shard == "tiles" else
                        (f"sample-parallel x{n}" + (" (RCCL reduce of the running means after the run)"

@@ -51,6 +51,7 @@ extern "C" {
 #define PT_FLAG_WAVEFRONT 0x8u    /* staged wavefront pipeline instead of the persistent megakernel */
 #define PT_FLAG_REGEN 0x10u       /* path-regeneration state-machine kernel instead of the megakernel */
 #define PT_FLAG_NO_TILE_ORDER 0x20u /* megakernel: hand out tiles in fixed order, not longest-first */
+#define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */
 
 typedef struct pt_config {
   int width;          /* RenderPass::width  (OpenglRayTracing/main.cpp:83), e.g. 1920 */
@@ -82,6 +83,8 @@ typedef struct pt_frame_stats {
   int max_stack;        /* traversal stack bound used (tree depth + 1) */
   int split_items;      /* megakernel: work items the next frame's schedule adds by splitting
                            long-path tiles (0 = one item per tile) */
+  int runtime_tree;     /* megakernel: 1 when the last frame traversed the runtime's own tree
+                           (results checked against the uploaded one), 0 the uploaded tree */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;

@@ -26,7 +26,7 @@ constexpr int LDS_NODES = PT_LDS_NODES;
 #define PT_SPLIT_PCT 25  // megakernel: split a tile whose longest item costs more than this % of a wave's share
 #endif
 #ifndef PT_SPLIT_AUTO
-#define PT_SPLIT_AUTO 1  // the runtime measures split vs unsplit after each running-mean restart (splitPolicy)
+#define PT_SPLIT_AUTO 1  // the runtime measures its tree and split policies after each running-mean restart (probePolicy)
 #endif
 #ifndef PT_WAVE_TRACE
 #define PT_WAVE_TRACE 0  // diagnostics build: record each megakernel wave's lifetime (tools/wave_trace.py)
@@ -47,6 +47,9 @@ constexpr size_t CTL_QUEUES = 0;                                      // NUM_QUE
 constexpr size_t CTL_STATS = 64 * 256;                                // 5 u64 cumulative fetch counters
 constexpr size_t CTL_RAYS = 65 * 256;                                 // RAY_SHARDS padded u64 counters
 constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
+#ifndef PT_FAST_TREE
+#define PT_FAST_TREE 1  // build and traverse the runtime's own tree (results checked against the reference's)
+#endif
 #ifndef PT_PACKETS
 #define PT_PACKETS 1  // megakernel: camera rays as wave packets (pt_trace.h tracePacket)
 #endif
@@ -66,6 +69,21 @@ struct SceneView {
   int nTop;            // device ids [0, nTop) are the top of the tree, staged in LDS by the megakernel
   int rootRef;         // encoded reference to node 1
   int nTri;
+  // The runtime's own tree over the same triangles (pt_runtime.cpp uploadAccel;
+  // pt_trace.h "Reference-exact results through the runtime's tree"): wide
+  // nodes with conservative boxes, pair records in its leaf order, and for
+  // every position the uploaded triangle index. fast = 0: not used this launch.
+  int fast;
+  const float4* fbvh;
+  const float4* fpairs;
+  const int* fastTri;
+  int fRoot, fnTop;
+  // reference facts: each triangle's reference leaf (-1 = none) and that leaf's
+  // box (lo, hi), every reference node's parent and box (lo, hi)
+  const int* refLeafOf;
+  const int* refParent;
+  const float4* refBox;
+  const float4* leafBox;
 };
 
 // HDR environment (hdrMap + hdrCache textures, IS main.cpp:843-853), float4 texels

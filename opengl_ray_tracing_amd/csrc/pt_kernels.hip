@@ -34,16 +34,40 @@ struct Tracer {
   const SceneView& S;
   Stack& st;
   Counters& C;
-  const float4* top;  // LDS copy of the top of the tree (null = none)
+  const float4* top;  // LDS copy of the top of the tree traversed first (null = none)
+  // closest hit: the triangle (-1 = miss) and its t. With S.fast, through the
+  // runtime's tree and checked against the reference's (pt_trace.h refReachable).
+  __device__ __forceinline__ int trace(V3 o, V3 d, float& t) {
+    if (!COUNT && S.fast) {
+      bool tie = false;
+      const SceneView F = fastView(S);
+      const int pos = traceRay<false, CULL, false, Stack, (LDS_NODES > 0), true>(F, o, d, t, st, C, false, top, &tie);
+      int tri = pos >= 0 ? S.fastTri[pos] : -1;
+      if (tie || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
+        C.rays--;  // the same ray, counted once
+        tri = traceRay<false, CULL, false, Stack>(S, o, d, t, st, C);
+      }
+      return tri;
+    }
+    return traceRay<false, CULL, COUNT, Stack, (LDS_NODES > 0)>(S, o, d, t, st, C, false, top);
+  }
   __device__ __forceinline__ bool closest(V3 o, V3 d, Hit& h) {
     float t;
-    int tri = traceRay<false, CULL, COUNT, Stack, (LDS_NODES > 0)>(S, o, d, t, st, C, false, top);
+    const int tri = trace(o, d, t);
     if (tri < 0) return false;
     finishHit(S, tri, o, d, t, h);
     return true;
   }
   __device__ __forceinline__ bool occluded(V3 o, V3 d) {
     float t;
+    if (!COUNT && S.fast) {
+      const SceneView F = fastView(S);
+      const int pos = traceRay<true, CULL, false, Stack, (LDS_NODES > 0)>(F, o, d, t, st, C, false, top);
+      if (pos < 0) return false;
+      if (refReachable(S, S.fastTri[pos], o, d, t)) return true;
+      C.rays--;
+      return traceRay<true, CULL, false, Stack>(S, o, d, t, st, C) >= 0;
+    }
     // COUNT reproduces the reference's closest-hit shadow query fetch by fetch
     return traceRay<!COUNT, CULL, COUNT, Stack, (LDS_NODES > 0)>(S, o, d, t, st, C, false, top) >= 0;
   }
@@ -209,7 +233,8 @@ __device__ __forceinline__ int primaryPixel(const RenderParams& p, int px, int p
   uint32_t seed;
   const V3 dir = cameraRay(p, px, py, seed);
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-  const int tri = traceRay<false, CULL, COUNT, Stack, (LDS_NODES > 0)>(p.scene, eye, dir, t, st, C, false, top);
+  Tracer<CULL, COUNT> tr{p.scene, st, C, top};
+  const int tri = tr.trace(eye, dir, t);
   if (tri < 0) {
     const V3 color = sampleHdr(p.env, dir);
     if (COUNT) C.texels++;
@@ -228,10 +253,20 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
   const V3 dir = cameraRay(p, valid ? px : 0, valid ? py : 0, seed);
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
   bool tie;
-  int tri = tracePacket<CULL>(p.scene, eye, dir, valid, t, tie, pstack, C, top);
-  if (valid && tie) {
-    C.rays--;  // the same ray, counted once
-    tri = traceRay<false, CULL, false, Stack, (LDS_NODES > 0)>(p.scene, eye, dir, t, st, C, false, top);
+  int tri;
+  if (p.scene.fast) {  // through the runtime's tree, checked against the reference's
+    const int pos = tracePacket<CULL>(fastView(p.scene), eye, dir, valid, t, tie, pstack, C, top);
+    tri = pos >= 0 ? p.scene.fastTri[pos] : -1;
+    if (valid && (tie || (tri >= 0 && !refReachable(p.scene, tri, eye, dir, t)))) {
+      C.rays--;  // the same ray, counted once
+      tri = traceRay<false, CULL, false, Stack>(p.scene, eye, dir, t, st, C);
+    }
+  } else {
+    tri = tracePacket<CULL>(p.scene, eye, dir, valid, t, tie, pstack, C, top);
+    if (valid && tie) {
+      C.rays--;
+      tri = traceRay<false, CULL, false, Stack, (LDS_NODES > 0)>(p.scene, eye, dir, t, st, C, false, top);
+    }
   }
   if (valid && tri < 0) {
     const V3 color = sampleHdr(p.env, dir);
@@ -543,7 +578,11 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
   // the top of the tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
   __shared__ float4 s_nodes[LDS_NODES * 4];
-  for (int i = threadIdx.x; i < p.scene.nTop * 4; i += BLOCK) s_nodes[i] = p.scene.bvh[i];
+  {
+    const float4* src = p.scene.fast ? p.scene.fbvh : p.scene.bvh;  // the tree traversed first
+    const int n = (p.scene.fast ? p.scene.fnTop : p.scene.nTop) * 4;
+    for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
+  }
   __syncthreads();
   const float4* top = s_nodes;
 #else

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "pt_abi.h"
+#include "pt_accel.h"
 #include "pt_fmath.h"
 #include "pt_kernels.h"
 #include "pt_scene.h"
@@ -41,6 +42,17 @@ struct pt_ctx {
   float* d_attr = nullptr;
   float4* d_bvh = nullptr;
   int nDevNodes = 0;  // internal nodes in d_bvh (device ids 0..nDevNodes-1)
+  // the runtime's own tree (uploadAccel; SceneView::fast) and the reference
+  // facts its results are checked against
+  bool fastReady = false;
+  float4* d_fbvh = nullptr;
+  float4* d_fpairs = nullptr;
+  int* d_fastTri = nullptr;
+  int* d_refLeafOf = nullptr;
+  int* d_refParent = nullptr;
+  float4* d_refBox = nullptr;
+  float4* d_leafBox = nullptr;
+  int fRoot = REF_NONE, fnDev = 0, fDepth = 0;
   int rootRef = REF_NONE;
   int nTri = 0, nNodes = 0, depth = 0, maxStack = 0;
   // env
@@ -58,11 +70,13 @@ struct pt_ctx {
   int* d_ovf = nullptr;
   int* d_cost = nullptr;   // per-tile cost of the last frame (megakernel)
   int* d_order = nullptr;  // per-band tile order for the next frame
-  // tile-split policy probe (splitPolicy): frames since the probe (re)started,
+  bool lastFast = false;    // the last megakernel frame traversed the runtime's tree
+  // tree / tile-split policy probe (probePolicy): frames since the probe (re)started,
   // the summed frame times of each policy, the decision
-  int probeFrame = 0, splitOnFrames = 0, splitOffFrames = 0;
-  double splitOnMs = 0.0, splitOffMs = 0.0;
-  int splitDecided = -1;   // -1 probing, 0 off, 1 on
+  int probeFrame = 0;
+  int probeN[3] = {0, 0, 0};           // timed frames: runtime tree, uploaded tree (both unsplit), split
+  double probeMs[3] = {0.0, 0.0, 0.0};
+  int treeDecided = -1, splitDecided = -1;  // -1 probing, 0 off, 1 on
   int orderCap = 0;        // work items per band in d_order
   bool orderValid = false;
   size_t ovfInts = 0;
@@ -100,6 +114,15 @@ template <class T>
 static void dfree(T*& p) {
   if (p) (void)hipFree((void*)p);
   p = nullptr;
+}
+
+template <class T>
+static int upload(pt_ctx* ctx, T** dst, const std::vector<T>& src) {
+  dfree(*dst);
+  if (src.empty()) return PT_OK;
+  CK(hipMalloc(dst, src.size() * sizeof(T)));
+  CK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return PT_OK;
 }
 
 extern "C" {
@@ -188,6 +211,8 @@ void pt_destroy(pt_ctx* ctx) {
   (void)hipSetDevice(ctx->cfg.device_id);
   if (ctx->own) (void)hipStreamSynchronize(ctx->own);
   dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
+  dfree(ctx->d_fbvh); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri); dfree(ctx->d_refLeafOf);
+  dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
@@ -209,24 +234,17 @@ static inline void nrm3(const float* a, const float* b, const float* c, float N[
   N[0] = cx * inv; N[1] = cy * inv; N[2] = cz * inv;
 }
 
-int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes, int nNodes) {
-  if (!ctx || !tris || !nodes) return PT_E_INVALID;
-  if (nTri < 1 || nNodes < 2) return fail(ctx, PT_E_BADSCENE, "need >= 1 triangle and >= 2 nodes (dummy 0, root 1)");
-  if (nTri > MAX_TRIS) return fail(ctx, PT_E_BADSCENE, "too many triangles for the leaf encoding");
-  CK(hipSetDevice(ctx->cfg.device_id));
-  // geometry records (+1 zero record: the leaf loop prefetches one record ahead)
-  std::vector<float4> geo((size_t)(nTri + 1) * 4, make_float4(0, 0, 0, 0));
-  for (int i = 0; i < nTri; i++) {
-    const float* t = tris + (size_t)i * 36;
-    float N[3];
-    nrm3(t, t + 3, t + 6, N);
-    float w = (N[0] * t[0] + N[1] * t[1]) + N[2] * t[2];
-    geo[4 * i + 0] = make_float4(t[0], t[1], t[2], w);
-    geo[4 * i + 1] = make_float4(t[3], t[4], t[5], 0.0f);
-    geo[4 * i + 2] = make_float4(t[6], t[7], t[8], 0.0f);
-    geo[4 * i + 3] = make_float4(N[0], N[1], N[2], 0.0f);
-  }
-  // node references (ivec3(texelFetch) truncation, pass1.fsh:238-243)
+// A tree in the reference node encoding (12 f32 per node, dummy node 0, root 1)
+// re-laid out as device wide nodes (pt_kernels.h SceneView::bvh). inflate > 0
+// widens every box outward by that relative amount plus inflateAbs (the
+// runtime's own tree: conservative, so a ray that hits a triangle always enters
+// its boxes).
+struct WideTree {
+  std::vector<float4> bvh;
+  int rootRef = REF_NONE, nDev = 0, depth = 0;
+};
+static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, float inflate, WideTree& out,
+                                  float inflateAbs = 0.0f) {
   auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
   auto isInternal = [&](int k) { return k > 0 && k < nNodes && nodeN(k) <= 0; };
   // depth of the reachable tree (bounds the traversal stack; rejects cycles)
@@ -237,7 +255,7 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
     while (!st.empty()) {
       auto [k, d] = st.back();
       st.pop_back();
-      if (++visits > 2L * nNodes) return fail(ctx, PT_E_BADSCENE, "node graph is not a tree (cycle)");
+      if (++visits > 2L * nNodes) return "node graph is not a tree (cycle)";
       depth = std::max(depth, d);
       if (nodeN(k) > 0) continue;
       int L = (int)nodes[(size_t)k * 12 + 0], R = (int)nodes[(size_t)k * 12 + 1];
@@ -248,8 +266,8 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
   // Device ids of the reachable internal nodes: the first LDS_NODES in
   // breadth-first order from the root (the top of the tree, which every ray
   // walks: the megakernel stages exactly these ids in LDS), the rest in the
-  // reference's id order (its preorder, which keeps subtrees together). Only
-  // the storage order changes; traversal visits the same nodes in the same
+  // tree's id order (the reference's preorder, which keeps subtrees together).
+  // Only the storage order changes; traversal visits the same nodes in the same
   // order.
   std::vector<int> newId(nNodes, -1), order;
   {
@@ -270,6 +288,7 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
     for (size_t i = 0; i < order.size(); i++) newId[order[i]] = (int)i;
   }
   std::string bad;
+  // node references (ivec3(texelFetch) truncation, pass1.fsh:238-243)
   auto encodeRef = [&](int k) -> int {
     if (k <= 0 || k >= nNodes) return REF_NONE;
     int n = nodeN(k);
@@ -281,22 +300,33 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
     }
     return newId[k];
   };
-  std::vector<float4> bvh(std::max<size_t>(order.size(), 1) * 4, make_float4(0, 0, 0, 0));
+  auto widen = [&](float4& lo, float4& hi) {
+    if (inflate <= 0.0f && inflateAbs <= 0.0f) return;
+    const float e[3] = {inflate * (std::fabs(lo.x) + std::fabs(hi.x) + (hi.x - lo.x)) + inflateAbs + 1e-30f,
+                        inflate * (std::fabs(lo.y) + std::fabs(hi.y) + (hi.y - lo.y)) + inflateAbs + 1e-30f,
+                        inflate * (std::fabs(lo.z) + std::fabs(hi.z) + (hi.z - lo.z)) + inflateAbs + 1e-30f};
+    lo.x -= e[0]; lo.y -= e[1]; lo.z -= e[2];
+    hi.x += e[0]; hi.y += e[1]; hi.z += e[2];
+  };
+  std::vector<float4>& bvh = out.bvh;
+  bvh.assign(std::max<size_t>(order.size(), 1) * 4, make_float4(0, 0, 0, 0));
   const float inf = INFINITY;
   for (size_t id = 0; id < order.size(); id++) {
     const int k = order[id];
     int L = (int)nodes[(size_t)k * 12 + 0], R = (int)nodes[(size_t)k * 12 + 1];
     int lr = encodeRef(L), rr = encodeRef(R);
-    if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
+    if (!bad.empty()) return bad;
     float4 la = make_float4(inf, inf, inf, 0), lb = make_float4(-inf, -inf, -inf, 0);
     float4 ra = la, rb = lb;
     if (lr != REF_NONE) {
       const float* c = nodes + (size_t)L * 12;
       la = make_float4(c[6], c[7], c[8], 0); lb = make_float4(c[9], c[10], c[11], 0);
+      widen(la, lb);
     }
     if (rr != REF_NONE) {
       const float* c = nodes + (size_t)R * 12;
       ra = make_float4(c[6], c[7], c[8], 0); rb = make_float4(c[9], c[10], c[11], 0);
+      widen(ra, rb);
     }
     // children paired per component (left, right) so one packed op serves both boxes
     float refs[2];
@@ -307,13 +337,22 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
     bvh[4 * id + 2] = make_float4(lb.y, rb.y, lb.z, rb.z);
     bvh[4 * id + 3] = make_float4(refs[0], refs[1], 0.0f, 0.0f);
   }
-  int rootRef = encodeRef(1);
-  if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
-  // pair records: triangle i (x) and i + 1 (y, zeros past the last), PAIR_F4 float4 each
-  std::vector<float4> pairs((size_t)nTri * PAIR_F4, make_float4(0, 0, 0, 0));
+  out.rootRef = encodeRef(1);
+  if (!bad.empty()) return bad;
+  out.nDev = (int)order.size();
+  out.depth = depth;
+  return "";
+}
+
+// pair records: position i holds triangles order[i] (x) and order[i + 1] (y,
+// zeros past the last), PAIR_F4 float4 each (pt_trace.h pairTest)
+static void buildPairs(const std::vector<float4>& geo, const int* order, int nTri, std::vector<float4>& pairs) {
+  pairs.assign((size_t)nTri * PAIR_F4, make_float4(0, 0, 0, 0));
+  const float4 zero[4] = {make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0),
+                          make_float4(0, 0, 0, 0)};
   for (int i = 0; i < nTri; i++) {
-    const float4* A = &geo[4 * (size_t)i];
-    const float4* B = &geo[4 * (size_t)(i + 1)];  // the zero record past the last triangle
+    const float4* A = &geo[4 * (size_t)(order ? order[i] : i)];
+    const float4* B = i + 1 < nTri ? &geo[4 * (size_t)(order ? order[i + 1] : i + 1)] : zero;
     float4* r = &pairs[(size_t)i * PAIR_F4];
     r[0] = make_float4(A[0].x, B[0].x, A[0].y, B[0].y);  // p1.x, p1.y
     r[1] = make_float4(A[0].z, B[0].z, A[1].x, B[1].x);  // p1.z, p2.x
@@ -323,22 +362,127 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
     r[5] = make_float4(A[3].y, B[3].y, A[3].z, B[3].z);  // Ng.y, Ng.z
     r[6] = make_float4(A[0].w, B[0].w, 0.0f, 0.0f);      // w = dot(Ng, p1)
   }
-  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
-  CK(hipMalloc(&ctx->d_pairs, pairs.size() * sizeof(float4)));
-  CK(hipMemcpy(ctx->d_pairs, pairs.data(), pairs.size() * sizeof(float4), hipMemcpyHostToDevice));
-  CK(hipMalloc(&ctx->d_geo, geo.size() * sizeof(float4)));
+}
+
+// The runtime's own tree (a binned-SAH build over the uploaded triangles) and
+// the reference facts a result found through it is checked against
+// (pt_trace.h refReachable): each triangle's reference leaf and its box, every
+// reference node's parent and box. Any triangle in two reference leaves, or a
+// failed build, leaves the runtime on the reference tree alone.
+static int uploadAccel(pt_ctx* ctx, const float* tris, int nTri, const float* nodes, int nNodes,
+                       const std::vector<float4>& geo) {
+  ctx->fastReady = false;
+  if (!PT_FAST_TREE) return PT_OK;
+  auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
+  std::vector<int> leafOf(nTri, -1), parent(nNodes, 0);
+  {
+    std::vector<int> st{1};
+    while (!st.empty()) {
+      const int k = st.back();
+      st.pop_back();
+      if (nodeN(k) > 0) {
+        const int index = (int)nodes[(size_t)k * 12 + 4];
+        for (int i = index; i < index + nodeN(k); i++) {
+          if (leafOf[i] != -1) return PT_OK;  // a triangle in two leaves: reference tree only
+          leafOf[i] = k;
+        }
+        continue;
+      }
+      for (int c = 0; c < 2; c++) {
+        const int ch = (int)nodes[(size_t)k * 12 + c];
+        if (ch > 0 && ch < nNodes) {
+          // refReachable's margin test needs every box inside its parent's (true
+          // of the reference builders, which bound each node's own triangles)
+          const float* pb = nodes + (size_t)k * 12;
+          const float* cb = nodes + (size_t)ch * 12;
+          for (int a = 0; a < 3; a++)
+            if (!(pb[6 + a] <= cb[6 + a] && cb[9 + a] <= pb[9 + a])) return PT_OK;
+          parent[ch] = k;
+          st.push_back(ch);
+        }
+      }
+    }
+  }
+  std::vector<float4> refBox((size_t)nNodes * 2), leafBox((size_t)nTri * 2);
+  for (int k = 0; k < nNodes; k++) {
+    const float* c = nodes + (size_t)k * 12;
+    refBox[2 * (size_t)k] = make_float4(c[6], c[7], c[8], 0.0f);
+    refBox[2 * (size_t)k + 1] = make_float4(c[9], c[10], c[11], 0.0f);
+  }
+  const float inf = INFINITY;
+  for (int i = 0; i < nTri; i++) {
+    if (leafOf[i] < 0) {  // in no reference leaf: never a reference hit (empty box fails the margin test)
+      leafBox[2 * (size_t)i] = make_float4(inf, inf, inf, 0.0f);
+      leafBox[2 * (size_t)i + 1] = make_float4(-inf, -inf, -inf, 0.0f);
+    } else {
+      leafBox[2 * (size_t)i] = refBox[2 * (size_t)leafOf[i]];
+      leafBox[2 * (size_t)i + 1] = refBox[2 * (size_t)leafOf[i] + 1];
+    }
+  }
+  std::vector<float> an;
+  std::vector<int> order;
+  if (pt::buildAccel(tris, nTri, 4, an, order) < 0 || an.size() / 12 >= (1u << 24)) return PT_OK;
+
+  // widened by 1e-5 of each box's own magnitude plus 3e-5 of the scene's: above
+  // the rounding of a slab test (~1.2e-7 x the origin-box distance) for ray origins
+  // up to ~100x the scene scale away, so a ray that hits a triangle enters every box around it
+  float sceneScale = 0.0f;
+  for (int i = 0; i < nTri; i++)
+    for (int k = 0; k < 9; k++) sceneScale = std::max(sceneScale, std::fabs(tris[(size_t)i * 36 + k]));
+  WideTree fast;
+  if (!encodeWideTree(an.data(), (int)(an.size() / 12), nTri, 1e-5f, fast, 3e-5f * sceneScale).empty()) return PT_OK;
+  std::vector<float4> fpairs;
+  buildPairs(geo, order.data(), nTri, fpairs);
+  int rc;
+  if ((rc = upload(ctx, &ctx->d_fbvh, fast.bvh)) || (rc = upload(ctx, &ctx->d_fpairs, fpairs)) ||
+      (rc = upload(ctx, &ctx->d_fastTri, order)) || (rc = upload(ctx, &ctx->d_refLeafOf, leafOf)) ||
+      (rc = upload(ctx, &ctx->d_refParent, parent)) || (rc = upload(ctx, &ctx->d_refBox, refBox)) ||
+      (rc = upload(ctx, &ctx->d_leafBox, leafBox)))
+    return rc;
+  ctx->fRoot = fast.rootRef;
+  ctx->fnDev = fast.nDev;
+  ctx->fDepth = fast.depth;
+  ctx->maxStack = std::max(ctx->maxStack, fast.depth + 1);
+  ctx->fastReady = true;
+  return PT_OK;
+}
+
+int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes, int nNodes) {
+  if (!ctx || !tris || !nodes) return PT_E_INVALID;
+  if (nTri < 1 || nNodes < 2) return fail(ctx, PT_E_BADSCENE, "need >= 1 triangle and >= 2 nodes (dummy 0, root 1)");
+  if (nTri > MAX_TRIS) return fail(ctx, PT_E_BADSCENE, "too many triangles for the leaf encoding");
+  CK(hipSetDevice(ctx->cfg.device_id));
+  // geometry records (+1 zero record past the last triangle)
+  std::vector<float4> geo((size_t)(nTri + 1) * 4, make_float4(0, 0, 0, 0));
+  for (int i = 0; i < nTri; i++) {
+    const float* t = tris + (size_t)i * 36;
+    float N[3];
+    nrm3(t, t + 3, t + 6, N);
+    float w = (N[0] * t[0] + N[1] * t[1]) + N[2] * t[2];
+    geo[4 * i + 0] = make_float4(t[0], t[1], t[2], w);
+    geo[4 * i + 1] = make_float4(t[3], t[4], t[5], 0.0f);
+    geo[4 * i + 2] = make_float4(t[6], t[7], t[8], 0.0f);
+    geo[4 * i + 3] = make_float4(N[0], N[1], N[2], 0.0f);
+  }
+  WideTree ref;
+  std::string bad = encodeWideTree(nodes, nNodes, nTri, 0.0f, ref);
+  if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
+  std::vector<float4> pairs;
+  buildPairs(geo, nullptr, nTri, pairs);
+  int rc;
+  if ((rc = upload(ctx, &ctx->d_pairs, pairs)) || (rc = upload(ctx, &ctx->d_geo, geo)) ||
+      (rc = upload(ctx, &ctx->d_bvh, ref.bvh)))
+    return rc;
+  dfree(ctx->d_attr);
   CK(hipMalloc(&ctx->d_attr, (size_t)nTri * 36 * sizeof(float)));
-  CK(hipMalloc(&ctx->d_bvh, bvh.size() * sizeof(float4)));
-  CK(hipMemcpy(ctx->d_geo, geo.data(), geo.size() * sizeof(float4), hipMemcpyHostToDevice));
   CK(hipMemcpy(ctx->d_attr, tris, (size_t)nTri * 36 * sizeof(float), hipMemcpyHostToDevice));
-  CK(hipMemcpy(ctx->d_bvh, bvh.data(), bvh.size() * sizeof(float4), hipMemcpyHostToDevice));
   ctx->nTri = nTri;
   ctx->nNodes = nNodes;
-  ctx->nDevNodes = (int)order.size();
-  ctx->rootRef = rootRef;
-  ctx->depth = depth;
-  ctx->maxStack = depth + 1;
-  return PT_OK;
+  ctx->nDevNodes = ref.nDev;
+  ctx->rootRef = ref.rootRef;
+  ctx->depth = ref.depth;
+  ctx->maxStack = ref.depth + 1;
+  return uploadAccel(ctx, tris, nTri, nodes, nNodes, geo);
 }
 
 // calculateHdrCache of host image hdr (w*h*3) into the device table out (w*h float4)
@@ -467,6 +611,16 @@ static SceneView sceneView(const pt_ctx* ctx) {
   s.nTop = std::min(LDS_NODES, ctx->nDevNodes);
   s.rootRef = ctx->rootRef;
   s.nTri = ctx->nTri;
+  s.fast = 0;  // set per launch (renderFrame)
+  s.fbvh = ctx->d_fbvh;
+  s.fpairs = ctx->d_fpairs;
+  s.fastTri = ctx->d_fastTri;
+  s.fRoot = ctx->fRoot;
+  s.fnTop = std::min(LDS_NODES, ctx->fnDev);
+  s.refLeafOf = ctx->d_refLeafOf;
+  s.refParent = ctx->d_refParent;
+  s.refBox = ctx->d_refBox;
+  s.leafBox = ctx->d_leafBox;
   return s;
 }
 
@@ -606,43 +760,54 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
   return PT_OK;
 }
 
-// Tile splitting (reorderKernel) pays off when the SIMDs have issue slots to
-// spare (the MIS integrator, latency-bound) and costs when they do not (the
-// Lambert megakernel is VALU-bound: a split item's idle lanes still take issue
-// cycles). Results are identical either way, so the runtime measures: after a
-// restart of the running mean (frameCounter 0, as on every camera move in the
-// reference) frames 1-2 run unsplit and 8-9 split (3-7 let the per-tile split
-// state converge), and the faster policy is kept until the next restart.
-// Returns the split percentage for this frame's reorder (0 = off).
-static int splitPolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered) {
-  if (!PT_SPLIT_AUTO || PT_SPLIT_PCT <= 0) return PT_SPLIT_PCT;
+// Two policies are chosen by measurement, since results are identical either
+// way and which is faster depends on the scene and the integrator:
+//  * the tree: the runtime's own (binned SAH; results checked against the
+//    uploaded tree) pays off when the uploaded tree is poor -- the reference's
+//    SAH with its z-typo: c2 0.57 -> 0.47 ms, c4 0.99 -> 0.80 -- and costs its
+//    checks when the uploaded tree is already good (c5: +2 %);
+//  * tile splitting (reorderKernel) pays off when the SIMDs have issue slots to
+//    spare (the MIS integrator, latency-bound) and costs when they do not (the
+//    Lambert megakernel is VALU-bound: a split item's idle lanes still take
+//    issue cycles).
+// After a restart of the running mean (frameCounter 0, as on every camera move
+// in the reference): frames 1-2 run the runtime's tree and 3-4 the uploaded
+// one, unsplit; the faster tree is kept; frames 5-11 split (5-9 let the
+// per-tile split state converge, 10-11 are timed) and the faster split policy
+// is kept until the next restart. Sets *useFast; returns the split percentage
+// for this frame's reorder (0 = off).
+static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast) {
+  *useFast = fastAllowed;
   if (!ordered) return 0;
+  if (!PT_SPLIT_AUTO) return PT_SPLIT_PCT;
   if (frameCounter == 0) {
     ctx->probeFrame = 0;
-    ctx->splitOnFrames = ctx->splitOffFrames = 0;
-    ctx->splitOnMs = ctx->splitOffMs = 0.0;
-    ctx->splitDecided = -1;
+    ctx->probeN[0] = ctx->probeN[1] = ctx->probeN[2] = 0;
+    ctx->probeMs[0] = ctx->probeMs[1] = ctx->probeMs[2] = 0.0;
+    ctx->treeDecided = ctx->splitDecided = -1;
     if (ctx->d_cost) (void)hipMemsetAsync(ctx->d_cost + 2 * (size_t)ctx->numItems, 0, (size_t)ctx->numItems * sizeof(int),
                                           ctx->stream);
   }
-  if (ctx->splitDecided >= 0) return ctx->splitDecided ? PT_SPLIT_PCT : 0;
-  // the previous frame's time (its launch is the last recorded one)
-  const int f = ctx->probeFrame++;
-  if (ctx->launches > 0 && (f == 2 || f == 3 || f == 9 || f == 10)) {
+  const int f = ctx->probeFrame < 1000 ? ctx->probeFrame++ : 1000;
+  // the previous frame's time (its launch is the last recorded one) into its probe slot
+  const int slot = (f == 2 || f == 3) ? 0 : (f == 4 || f == 5) ? 1 : (f == 11 || f == 12) ? 2 : -1;
+  if (slot >= 0 && ctx->launches > 0 && ctx->splitDecided < 0) {
     float ms = 0.0f;
     hipEvent_t b = ctx->evs[2 * (ctx->launches - 1)], e = ctx->evs[2 * (ctx->launches - 1) + 1];
     if (hipEventSynchronize(e) == hipSuccess && hipEventElapsedTime(&ms, b, e) == hipSuccess) {
-      if (f <= 3) { ctx->splitOffMs += ms; ctx->splitOffFrames++; }
-      else { ctx->splitOnMs += ms; ctx->splitOnFrames++; }
+      ctx->probeMs[slot] += ms;
+      ctx->probeN[slot]++;
     }
   }
-  if (f >= 10) {
-    const bool on = ctx->splitOnFrames > 0 && ctx->splitOffFrames > 0 &&
-                    ctx->splitOnMs / ctx->splitOnFrames < ctx->splitOffMs / ctx->splitOffFrames;
-    ctx->splitDecided = on ? 1 : 0;
-    return on ? PT_SPLIT_PCT : 0;
-  }
-  return f >= 3 ? PT_SPLIT_PCT : 0;
+  auto avg = [&](int k) { return ctx->probeN[k] ? ctx->probeMs[k] / ctx->probeN[k] : 1e30; };
+  if (f == 5 && ctx->treeDecided < 0) ctx->treeDecided = fastAllowed && avg(0) <= avg(1) ? 1 : 0;
+  if (f == 12 && ctx->splitDecided < 0) ctx->splitDecided = PT_SPLIT_PCT > 0 && avg(2) < avg(ctx->treeDecided ? 0 : 1) ? 1 : 0;
+  // this frame's tree
+  if (ctx->treeDecided >= 0) *useFast = fastAllowed && ctx->treeDecided;
+  else *useFast = fastAllowed && f <= 2;
+  // this frame's split policy (for the next frame's items)
+  if (ctx->splitDecided >= 0) return ctx->splitDecided ? PT_SPLIT_PCT : 0;
+  return f >= 5 ? PT_SPLIT_PCT : 0;
 }
 
 int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
@@ -715,7 +880,8 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   p.world = c.tile_world;
   p.ovf = ovfDepth ? ctx->d_ovf : nullptr;
   p.ovfDepth = ovfDepth;
-  p.packets = PT_PACKETS && ctx->maxStack <= PKT_DEPTH;
+  p.scene.fast = 0;  // probePolicy below
+
   p.stats = stats;
   p.rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAYS);
   // longest-tiles-first: each band's tiles in the order of the previous frame's cost
@@ -732,7 +898,14 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
     CK(hipMalloc(&ctx->d_order, ((size_t)NUM_QUEUES * orderCap + NUM_QUEUES) * sizeof(int)));
     ctx->orderValid = false;
   }
-  const int splitPct = splitPolicy(ctx, frameCounter, ordered);
+  // the tree (the runtime's own, checked against the uploaded one, unless asked
+  // not to) and the split policy: probePolicy
+  bool useFast = false;
+  const int splitPct = probePolicy(ctx, frameCounter, ordered,
+                                   !count && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast);
+  p.scene.fast = useFast ? 1 : 0;
+  ctx->lastFast = useFast;
+  p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
   p.tileOrder = ordered && ctx->orderValid ? ctx->d_order : nullptr;
   p.orderCap = orderCap;
   p.tileCost = ordered ? ctx->d_cost : nullptr;
@@ -935,6 +1108,7 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   st->launches = ctx->launches;
   st->max_stack = ctx->maxStack;
   st->split_items = 0;
+  st->runtime_tree = ctx->lastFast ? 1 : 0;
   if (ctx->d_order && ctx->orderValid) {
     int counts[NUM_QUEUES];
     CK(hipMemcpy(counts, ctx->d_order + (size_t)NUM_QUEUES * ctx->orderCap, sizeof(counts), hipMemcpyDeviceToHost));

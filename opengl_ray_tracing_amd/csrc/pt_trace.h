@@ -182,9 +182,12 @@ __device__ __forceinline__ bool isLeafRef(int ref) { return ref < 0 && ref != RE
 // top (LDSTOP): the LDS copy of device node ids [0, S.nTop) -- the top of the
 // tree -- read in place of the global records (one flat load serves lanes in
 // both address spaces).
-template <bool ANYHIT, bool CULL, bool COUNT, class StackType, bool LDSTOP = false>
+//
+// TIES: *tie is set when a lane meets a triangle at exactly its current closest
+// t (the visiting order decides such ties; see refReachable).
+template <bool ANYHIT, bool CULL, bool COUNT, class StackType, bool LDSTOP = false, bool TIES = false>
 __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
-                                        bool anyRT = false, const float4* top = nullptr) {
+                                        bool anyRT = false, const float4* top = nullptr, bool* tie = nullptr) {
   V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float tbest = PT_INF;
   int best = -1;
@@ -267,11 +270,13 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
           if (h1 && t1 < localBest) { localBest = t1; C.mats++; }
           if (h1 && t1 < tbest) { tbest = t1; best = i + 1; }
         } else {
+          if (TIES && g0 && t0 == tbest) *tie = true;
           if (g0 && t0 < tbest) {
             tbest = t0;
             best = i;
             if (ANYHIT || anyRT) { tOut = tbest; return best; }
           }
+          if (TIES && g1 && second && t1 == tbest) *tie = true;
           if (g1 && second && t1 < tbest) {
             tbest = t1;
             best = i + 1;
@@ -283,6 +288,53 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
   }
   tOut = tbest;
   return best;
+}
+
+// ----------------------------------------------------------------- reference-exact results
+// Reference-exact results through the runtime's tree. The reference's closest
+// hit is the first, in its traversal order, of the triangles with the least t
+// among those its traversal reaches; it reaches a triangle iff the ray's
+// hitAABB is > 0 for every box on the path from the root to the triangle's
+// leaf. The runtime's tree has conservative (widened) boxes, so its traversal
+// meets every triangle the ray hits. Its result w (least t, no tie met) is
+// therefore the reference's iff the reference reaches w, which refReachable
+// decides: cheaply when the hit point lies inside w's reference leaf box by a
+// margin far above the rounding of the slab arithmetic (the exact ray then
+// crosses every enclosing box with room to spare, so every rounded slab test on
+// the path passes), else by evaluating hitAABB up the reference path. A tie, or
+// an unreachable w, sends the ray through the reference traversal itself.
+// A miss in the runtime's tree is a miss in the reference's (it meets every
+// triangle the ray hits). An any-hit result stands when its triangle is reachable.
+__device__ __forceinline__ bool refReachable(const SceneView& S, int tri, V3 o, V3 d, float t) {
+  const int leaf = S.refLeafOf[tri];
+  if (leaf < 0) return false;
+  const V3 P = o + d * t;
+  const float4 lo = S.leafBox[2 * (size_t)tri], hi = S.leafBox[2 * (size_t)tri + 1];
+  const float scale = fmaxf(fmaxf(fabsf(P.x), fmaxf(fabsf(P.y), fabsf(P.z))),
+                            fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)))) +
+                      fmaxf(fmaxf(fmaxf(fabsf(lo.x), fabsf(hi.x)), fmaxf(fabsf(lo.y), fabsf(hi.y))),
+                            fmaxf(fabsf(lo.z), fabsf(hi.z))) +
+                      t + 1.0f;
+  const float mu = 6.103515625e-05f * scale;  // 2^-14: >= 2^8 x the slab rounding
+  if (P.x - lo.x > mu && hi.x - P.x > mu && P.y - lo.y > mu && hi.y - P.y > mu && P.z - lo.z > mu &&
+      hi.z - P.z > mu)
+    return true;
+  const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  for (int c = leaf; c != 1; c = S.refParent[c]) {
+    if (c <= 0) return false;
+    float t0;
+    if (!(hitAABB(o, inv, S.refBox[2 * (size_t)c], S.refBox[2 * (size_t)c + 1], t0) > 0.0f)) return false;
+  }
+  return true;
+}
+// the runtime's tree as a SceneView for traceRay / tracePacket
+__device__ __forceinline__ SceneView fastView(const SceneView& S) {
+  SceneView F = S;
+  F.bvh = S.fbvh;
+  F.pairs = S.fpairs;
+  F.rootRef = S.fRoot;
+  F.nTop = S.fnTop;
+  return F;
 }
 
 // ----------------------------------------------------------------- camera-ray packets

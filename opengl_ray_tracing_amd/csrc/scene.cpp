@@ -4,6 +4,7 @@
 // order the reference's glm 0.9.9.8 code performs it, so the encoded arrays
 // match what the reference host program would upload (OpenglRayTracing/main.cpp).
 #include "pt_scene.h"
+#include "pt_accel.h"
 
 #include <algorithm>
 #include <cmath>
@@ -152,6 +153,7 @@ Material from_pt(const pt_material* m) {
 struct Triangle {  // main.cpp:45-49
   f3 p1, p2, p3, n1, n2, n3;
   Material material;
+  int id = 0;  // uploaded index (buildAccel only)
 };
 struct BVHNode {  // main.cpp:63-67
   int left, right, n, index;
@@ -419,6 +421,39 @@ int tree_depth(const std::vector<BVHNode>& nodes) {
 }
 
 }  // namespace
+
+int pt::buildAccel(const float* tris, int nTri, int leafSize, std::vector<float>& out, std::vector<int>& order) {
+  if (!tris || nTri < 1 || leafSize < 1) return -1;
+  std::vector<Triangle> tr((size_t)nTri);
+  for (int i = 0; i < nTri; i++) {
+    const float* t = tris + (size_t)i * 36;
+    tr[i].p1 = F3(t[0], t[1], t[2]);
+    tr[i].p2 = F3(t[3], t[4], t[5]);
+    tr[i].p3 = F3(t[6], t[7], t[8]);
+    tr[i].id = i;
+  }
+  std::vector<BVHNode> nodes(1);
+  nodes[0] = BVHNode{0, 0, 0, 0, F3(0, 0, 0), F3(0, 0, 0)};
+  nodes.reserve(2 * (size_t)nTri / (size_t)leafSize + 16);
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  int parDepth = 0;
+  while ((1u << parDepth) < hw) parDepth++;
+  buildTree(tr, nodes, 0, nTri - 1, leafSize, splitBinned, false, parDepth);
+  out.assign(nodes.size() * 12, 0.0f);
+  for (size_t i = 0; i < nodes.size(); i++) {
+    const BVHNode& n = nodes[i];
+    float* o = out.data() + i * 12;
+    o[0] = (float)n.left;
+    o[1] = (float)n.right;
+    o[3] = (float)n.n;
+    o[4] = (float)n.index;
+    o[6] = n.AA.x; o[7] = n.AA.y; o[8] = n.AA.z;
+    o[9] = n.BB.x; o[10] = n.BB.y; o[11] = n.BB.z;
+  }
+  order.resize((size_t)nTri);
+  for (int i = 0; i < nTri; i++) order[i] = tr[i].id;
+  return tree_depth(nodes);
+}
 
 struct pt_scene {
   std::vector<Triangle> triangles;

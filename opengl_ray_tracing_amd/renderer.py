@@ -31,6 +31,7 @@ FLAG_COUNT_FETCHES = 0x4
 FLAG_WAVEFRONT = 0x8
 FLAG_REGEN = 0x10
 FLAG_NO_TILE_ORDER = 0x20
+FLAG_REFERENCE_TREE = 0x40
 
 
 @dataclass
@@ -45,6 +46,7 @@ class FrameStats:
     launches: int
     max_stack: int
     split_items: int
+    runtime_tree: int
 
 
 def _fp(a: np.ndarray):
@@ -193,7 +195,7 @@ class Renderer:
         s = _native.PtFrameStats()
         self._ck(self._lib.pt_get_stats(self._h, C.byref(s)), "pt_get_stats")
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
-                          s.kernel_ms_total, s.launches, s.max_stack, s.split_items)
+                          s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

@@ -129,6 +129,21 @@ def test_frame_kernels_agree(request, name, integrator):
         assert sa.rays == sb.rays == sc.rays
 
 
+@pytest.mark.parametrize("name,integrator", [("c2", "lambert"), ("c3", "disney"), ("c3", "mis"), ("c4", "mis")])
+def test_runtime_tree_equals_reference_tree(request, name, integrator):
+    """Traversing the runtime's own tree (a binned-SAH build; results checked against the
+    uploaded tree and retraced through it on a tie or an unreachable hit) gives the image of
+    the uploaded reference tree bit for bit, with the same rays, over several frames."""
+    from opengl_ray_tracing_amd import FLAG_REFERENCE_TREE
+    cfg, tris, nodes, hdr = request.getfixturevalue(name)
+    mb = {"disney": 5}.get(integrator, cfg.max_bounce)
+    a, sa = render_gpu(cfg, tris, nodes, hdr, frames=3, integrator=integrator, max_bounce=mb)
+    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=3, integrator=integrator, max_bounce=mb,
+                       flags=FLAG_REFERENCE_TREE)
+    assert np.array_equal(a, b)
+    assert sa.rays == sb.rays
+
+
 def test_tile_splitting_does_not_change_the_image(c4):
     """Long-path tiles split into smaller work items (frames 4-10 after a restart, while the
     runtime probes the split policy) only regroup lanes: the image equals the fixed-order,
