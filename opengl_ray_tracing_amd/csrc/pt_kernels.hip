@@ -682,11 +682,15 @@ __global__ __launch_bounds__(BLOCK) void traceKernel(TraceParams p) {
   const size_t gtid = (size_t)blockIdx.x * BLOCK + threadIdx.x;
   st.gbl = p.ovf ? p.ovf + gtid * p.ovfDepth : nullptr;
   Counters C = {0, 0, 0, 0, 0};
+  SceneView S = p.scene;  // no LDS copy of the top of the tree here
+  S.nTop = 0;
+  S.fnTop = 0;
+  Tracer<CULL, false> tr{S, st, C, nullptr};  // the runtime's tree when S.fast (reference-exact)
   for (size_t k = gtid; k < (size_t)p.n; k += (size_t)gridDim.x * BLOCK) {
     const float* r = p.rays + 6 * k;
     V3 o = v3(r[0], r[1], r[2]), d = v3(r[3], r[4], r[5]);
     float t;
-    int tri = traceRay<false, CULL, false>(p.scene, o, d, t, st, C);
+    int tri = tr.trace(o, d, t);
     p.t[k] = tri >= 0 ? t : PT_INF;
     p.tri[k] = tri;
   }

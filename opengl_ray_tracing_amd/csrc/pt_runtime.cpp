@@ -977,6 +977,8 @@ int pt_trace_closest(pt_ctx* ctx, const float* rays, int n, float* t_out, int* t
   CK(hipMemcpyAsync(ctx->d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
   TraceParams p;
   p.scene = sceneView(ctx);
+  // the runtime's own tree, results reference-exact (pt_trace.h refReachable)
+  p.scene.fast = ctx->fastReady && !(ctx->cfg.flags & (PT_FLAG_REFERENCE_TREE | PT_FLAG_COUNT_FETCHES)) ? 1 : 0;
   p.rays = ctx->d_rays;
   p.n = n;
   p.t = ctx->d_t;

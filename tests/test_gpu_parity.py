@@ -39,7 +39,7 @@ def random_rays(eye, n, seed):
     return np.concatenate([o, d], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("flags", [0, FLAG_NO_CULL])
+@pytest.mark.parametrize("flags", [0, FLAG_NO_CULL, 0x40])  # 0x40 = FLAG_REFERENCE_TREE
 def test_trace_closest_bit_exact(c2, flags):
     cfg, tris, nodes, hdr = c2
     orc = oracle.Oracle(tris, nodes)
@@ -49,6 +49,39 @@ def test_trace_closest_bit_exact(c2, flags):
         r.upload_scene(tris, nodes)
         t, tri = r.trace_closest(rays)
     t_o, tri_o, _ = orc.trace_closest(rays)
+    assert (tri_o >= 0).mean() > 0.2
+    assert np.array_equal(tri, tri_o)
+    assert np.array_equal(t, t_o)
+
+
+def test_trace_closest_exact_ties():
+    """Every triangle twice, so every hit is an exact-t tie decided by the reference's
+    visiting order: the runtime tree flags the ties and retraces those rays through the
+    uploaded tree, giving the oracle's triangle for every ray."""
+    from opengl_ray_tracing_amd import Material, Scene
+    n = 24
+    u, v = np.meshgrid(np.linspace(-1, 1, n), np.linspace(-1, 1, n))
+    verts = np.stack([u.ravel(), 0.2 * np.sin(3 * u.ravel()) * np.cos(2 * v.ravel()), v.ravel()], 1)
+    idx = []
+    for i in range(n - 1):
+        for j in range(n - 1):
+            a = i * n + j
+            idx += [[a, a + 1, a + n], [a + 1, a + n + 1, a + n]]
+    idx = np.array(idx, np.int32)
+    s = Scene()
+    s.add_mesh(verts.astype(np.float32), idx, Material())
+    s.add_mesh(verts.astype(np.float32), idx, Material())
+    s.build_bvh("sah", 8)
+    tris, nodes = s.encode()
+    rng = np.random.default_rng(7)
+    o = np.stack([rng.uniform(-0.8, 0.8, 20000), np.full(20000, 2.0), rng.uniform(-0.8, 0.8, 20000)], 1)
+    d = np.stack([rng.normal(0, 0.2, 20000), -np.ones(20000), rng.normal(0, 0.2, 20000)], 1)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    with Renderer(64, 64, "lambert") as r:
+        r.upload_scene(tris, nodes)
+        t, tri = r.trace_closest(rays)
+    t_o, tri_o, _ = oracle.Oracle(tris, nodes).trace_closest(rays)
     assert (tri_o >= 0).mean() > 0.2
     assert np.array_equal(tri, tri_o)
     assert np.array_equal(t, t_o)
