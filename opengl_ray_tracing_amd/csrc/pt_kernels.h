@@ -50,6 +50,9 @@ constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
 #ifndef PT_FAST_TREE
 #define PT_FAST_TREE 1  // build and traverse the runtime's own tree (results checked against the reference's)
 #endif
+#ifndef PT_ACCEL_LEAF
+#define PT_ACCEL_LEAF 4  // most triangles per leaf of the runtime's tree
+#endif
 #ifndef PT_PACKETS
 #define PT_PACKETS 1  // megakernel: camera rays as wave packets (pt_trace.h tracePacket)
 #endif

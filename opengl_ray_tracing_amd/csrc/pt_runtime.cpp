@@ -421,7 +421,7 @@ static int uploadAccel(pt_ctx* ctx, const float* tris, int nTri, const float* no
   }
   std::vector<float> an;
   std::vector<int> order;
-  if (pt::buildAccel(tris, nTri, 4, an, order) < 0 || an.size() / 12 >= (1u << 24)) return PT_OK;
+  if (pt::buildAccel(tris, nTri, PT_ACCEL_LEAF, an, order) < 0 || an.size() / 12 >= (1u << 24)) return PT_OK;
 
   // widened by 1e-5 of each box's own magnitude plus 3e-5 of the scene's: above
   // the rounding of a slab test (~1.2e-7 x the origin-box distance) for ray origins

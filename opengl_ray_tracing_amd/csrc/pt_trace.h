@@ -490,10 +490,12 @@ struct Hit {
   Material m;
 };
 __device__ __forceinline__ void finishHit(const SceneView& S, int tri, V3 o, V3 d, float t, Hit& h) {
-  const float4* g = S.geo + 4 * (size_t)tri;
-  float4 A = g[0], B = g[1], C4 = g[2], Nn = g[3];
-  V3 p1 = v3(A.x, A.y, A.z), p2 = v3(B.x, B.y, B.z), p3 = v3(C4.x, C4.y, C4.z);
-  bool inside = dot(v3(Nn.x, Nn.y, Nn.z), d) > 0.0f;
+  // the triangle's vertices and normal from its pair record (the x halves), the
+  // record the leaf test of an uploaded-tree traversal has just read
+  const float4* pr = S.pairs + PAIR_F4 * (size_t)tri;
+  const float4 r0 = pr[0], r1 = pr[1], r2 = pr[2], r3 = pr[3], r4 = pr[4], r5 = pr[5];
+  V3 p1 = v3(r0.x, r0.z, r1.x), p2 = v3(r1.z, r2.x, r2.z), p3 = v3(r3.x, r3.z, r4.x);
+  bool inside = dot(v3(r4.z, r5.x, r5.z), d) > 0.0f;
   V3 P = o + d * t;
   float alpha = (-(P.x - p2.x) * (p3.y - p2.y) + (P.y - p2.y) * (p3.x - p2.x)) /
                 (-(p1.x - p2.x - 0.00005f) * (p3.y - p2.y + 0.00005f) + (p1.y - p2.y + 0.00005f) * (p3.x - p2.x + 0.00005f));
