@@ -8,7 +8,7 @@ TAG="${1:-r1}"; CFG="${2:-c2}"; FLAGS="${3:-0}"
 OUT="$REPO/gpurun_out/pmc_${TAG}_${CFG}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-RUN=(python3 "$REPO/tools/tune.py" --child base --config "$CFG" --frames 5 --warmup 2 --flags "$FLAGS" ${MB:+--max-bounce $MB})
+RUN=(python3 "$REPO/tools/tune.py" --child base --config "$CFG" --frames 5 --warmup 16 --flags "$FLAGS" ${MB:+--max-bounce $MB})
 PASSES=(
   "A:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
   "B:SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VMEM"
