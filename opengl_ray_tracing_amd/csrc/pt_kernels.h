@@ -50,6 +50,10 @@ constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
 #ifndef PT_FAST_TREE
 #define PT_FAST_TREE 1  // build and traverse the runtime's own tree (results checked against the reference's)
 #endif
+#ifndef PT_QUANT_NODES
+#define PT_QUANT_NODES 0  // 1: the runtime tree's node records quantized to 8 bits per plane (measured slower: DESIGN.md)
+#endif
+constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
 #ifndef PT_ACCEL_LEAF
 #define PT_ACCEL_LEAF 4  // most triangles per leaf of the runtime's tree
 #endif

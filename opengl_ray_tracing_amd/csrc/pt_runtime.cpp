@@ -242,9 +242,46 @@ static inline void nrm3(const float* a, const float* b, const float* c, float N[
 struct WideTree {
   std::vector<float4> bvh;
   int rootRef = REF_NONE, nDev = 0, depth = 0;
+  bool quant = false;  // 3-float4 quantized records (pt_trace.h visitNodeQ) instead of 4-float4 exact ones
 };
+
+// One axis of a quantized node: origin o and scale 2^k for the planes of both
+// children, then each plane rounded one step outward beyond its own rounding
+// (pt_trace.h visitNodeQ decodes origin + q * 2^k with one rounding of the add).
+static bool quantAxis(const float* lo, const float* hi, const bool* valid, float& o, int& kOut, uint8_t q[4]) {
+  float mn = INFINITY, mx = -INFINITY;
+  for (int c = 0; c < 2; c++)
+    if (valid[c]) { mn = std::min(mn, lo[c]); mx = std::max(mx, hi[c]); }
+  if (!(mn <= mx)) { o = 0.0f; kOut = 0; q[0] = q[1] = q[2] = q[3] = 0; return true; }
+  o = mn;
+  const double e = (double)mx - (double)mn;
+  const float mag = std::max(std::fabs(mn), std::fabs(mx));
+  int E = 0;
+  std::frexp(mag > 0.0f ? mag : 1e-30f, &E);  // mag in [2^(E-1), 2^E)
+  int k = (E - 1) - 23 + 2;                    // 2^k >= 4 ulp(mag)
+  if (e > 0.0) k = std::max(k, (int)std::ceil(std::log2(e / 250.0)));
+  k = std::max(k, -126);
+  if (k > 127) return false;
+  const double sc = std::ldexp(1.0, k);
+  const float sf = (float)sc;
+  for (int c = 0; c < 2; c++) {
+    uint8_t* ql = &q[2 * c];
+    if (!valid[c]) { ql[0] = ql[1] = 0; continue; }
+    long a = (long)std::floor(((double)lo[c] - o) / sc) - 1, b = (long)std::ceil(((double)hi[c] - o) / sc) + 1;
+    a = std::max(0L, a);
+    b = std::min(255L, b);
+    // the device's decode, checked: a plane may only move outward
+    while (a > 0 && !(o + (float)a * sf <= lo[c])) a--;
+    while (b < 255 && !(o + (float)b * sf >= hi[c])) b++;
+    if (!(o + (float)a * sf <= lo[c]) || !(o + (float)b * sf >= hi[c])) return false;
+    ql[0] = (uint8_t)a;
+    ql[1] = (uint8_t)b;
+  }
+  kOut = k;
+  return true;
+}
 static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, float inflate, WideTree& out,
-                                  float inflateAbs = 0.0f) {
+                                  float inflateAbs = 0.0f, bool quantize = false) {
   auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
   auto isInternal = [&](int k) { return k > 0 && k < nNodes && nodeN(k) <= 0; };
   // depth of the reachable tree (bounds the traversal stack; rejects cycles)
@@ -309,7 +346,9 @@ static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, floa
     hi.x += e[0]; hi.y += e[1]; hi.z += e[2];
   };
   std::vector<float4>& bvh = out.bvh;
-  bvh.assign(std::max<size_t>(order.size(), 1) * 4, make_float4(0, 0, 0, 0));
+  const int F4 = quantize ? 3 : 4;
+  out.quant = quantize;
+  bvh.assign(std::max<size_t>(order.size(), 1) * F4, make_float4(0, 0, 0, 0));
   const float inf = INFINITY;
   for (size_t id = 0; id < order.size(); id++) {
     const int k = order[id];
@@ -332,6 +371,32 @@ static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, floa
     float refs[2];
     std::memcpy(&refs[0], &lr, 4);
     std::memcpy(&refs[1], &rr, 4);
+    if (quantize) {
+      const bool valid[2] = {lr != REF_NONE, rr != REF_NONE};
+      const float los[3][2] = {{la.x, ra.x}, {la.y, ra.y}, {la.z, ra.z}};
+      const float his[3][2] = {{lb.x, rb.x}, {lb.y, rb.y}, {lb.z, rb.z}};
+      float o[3];
+      int k[3];
+      uint8_t q[3][4];  // per axis: L.lo, L.hi, R.lo, R.hi
+      for (int a = 0; a < 3; a++)
+        if (!quantAxis(los[a], his[a], valid, o[a], k[a], q[a])) return "quantize";
+      // plane bytes L.lo.xyz L.hi.xyz R.lo.xyz R.hi.xyz, then the left ref
+      const uint8_t b[12] = {q[0][0], q[1][0], q[2][0], q[0][1], q[1][1], q[2][1],
+                             q[0][2], q[1][2], q[2][2], q[0][3], q[1][3], q[2][3]};
+      uint32_t w[3], ebits = 0;
+      std::memcpy(w, b, 12);
+      for (int a = 0; a < 3; a++) ebits |= (uint32_t)(k[a] + 127) << (8 * a);
+      float fw[4];
+      std::memcpy(&fw[0], &w[0], 4);
+      std::memcpy(&fw[1], &w[1], 4);
+      std::memcpy(&fw[2], &w[2], 4);
+      float fe;
+      std::memcpy(&fe, &ebits, 4);
+      bvh[3 * id + 0] = make_float4(o[0], o[1], o[2], fe);
+      bvh[3 * id + 1] = make_float4(fw[0], fw[1], fw[2], refs[0]);
+      bvh[3 * id + 2] = make_float4(refs[1], 0.0f, 0.0f, 0.0f);
+      continue;
+    }
     bvh[4 * id + 0] = make_float4(la.x, ra.x, la.y, ra.y);
     bvh[4 * id + 1] = make_float4(la.z, ra.z, lb.x, rb.x);
     bvh[4 * id + 2] = make_float4(lb.y, rb.y, lb.z, rb.z);
@@ -430,7 +495,9 @@ static int uploadAccel(pt_ctx* ctx, const float* tris, int nTri, const float* no
   for (int i = 0; i < nTri; i++)
     for (int k = 0; k < 9; k++) sceneScale = std::max(sceneScale, std::fabs(tris[(size_t)i * 36 + k]));
   WideTree fast;
-  if (!encodeWideTree(an.data(), (int)(an.size() / 12), nTri, 1e-5f, fast, 3e-5f * sceneScale).empty()) return PT_OK;
+  // (a tree whose planes do not quantize is not used: the traversal's record kind is FAST_QUANT)
+  if (!encodeWideTree(an.data(), (int)(an.size() / 12), nTri, 1e-5f, fast, 3e-5f * sceneScale, FAST_QUANT).empty())
+    return PT_OK;
   std::vector<float4> fpairs;
   buildPairs(geo, order.data(), nTri, fpairs);
   int rc;

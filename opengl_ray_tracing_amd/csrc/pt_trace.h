@@ -77,12 +77,11 @@ struct NodeHit {
   float t0l, t0r;  // slab entries (culling)
   int lref, rref;
 };
-__device__ __forceinline__ void visitNode(const float4* nd, V3 o, V3 inv, NodeHit& h) {
-  const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+// the slab tests of both children from their boxes as float pairs
+__device__ __forceinline__ void slabPair(f32x2 lox, f32x2 loy, f32x2 loz, f32x2 hix, f32x2 hiy, f32x2 hiz, V3 o, V3 inv,
+                                         NodeHit& h) {
   const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
   const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-  const f32x2 lox = {q0.x, q0.y}, loy = {q0.z, q0.w}, loz = {q1.x, q1.y};
-  const f32x2 hix = {q1.z, q1.w}, hiy = {q2.x, q2.y}, hiz = {q2.z, q2.w};
   const f32x2 fx = (hix - ox) * ix, fy = (hiy - oy) * iy, fz = (hiz - oz) * iz;
   const f32x2 nx = (lox - ox) * ix, ny = (loy - oy) * iy, nz = (loz - oz) * iz;
   float t1 = fminf(fmaxf(fx.x, nx.x), fminf(fmaxf(fy.x, ny.x), fmaxf(fz.x, nz.x)));
@@ -93,9 +92,49 @@ __device__ __forceinline__ void visitNode(const float4* nd, V3 o, V3 inv, NodeHi
   t0 = fmaxf(fminf(fx.y, nx.y), fmaxf(fminf(fy.y, ny.y), fminf(fz.y, nz.y)));
   h.t0r = t0;
   h.d2 = (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
+}
+__device__ __forceinline__ void visitNode(const float4* nd, V3 o, V3 inv, NodeHit& h) {
+  const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+  const f32x2 lox = {q0.x, q0.y}, loy = {q0.z, q0.w}, loz = {q1.x, q1.y};
+  const f32x2 hix = {q1.z, q1.w}, hiy = {q2.x, q2.y}, hiz = {q2.z, q2.w};
+  slabPair(lox, loy, loz, hix, hiy, hiz, o, inv, h);
   h.lref = __float_as_int(q3.x);
   h.rref = __float_as_int(q3.y);
 }
+// The runtime tree's quantized node (pt_runtime.cpp encodeWideTree, 36 of its
+// 48 bytes read): {origin.xyz, per-axis scale exponents}, 12 plane bytes
+// (L.lo.xyz L.hi.xyz R.lo.xyz R.hi.xyz) + left ref, {right ref}. A plane is
+// origin + q * 2^k: the multiply is exact, the add rounds once, and the host
+// rounded every plane one step outward beyond that, so the decoded boxes
+// contain the exact ones (whose results refReachable checks anyway).
+__device__ __forceinline__ float qscale(uint32_t bits, int axis) {
+  return __uint_as_float(((bits >> (8 * axis)) & 255u) << 23);  // 2^(byte - 127)
+}
+__device__ __forceinline__ void visitNodeQ(const float4* nd, V3 o, V3 inv, NodeHit& h) {
+  const float4 c0 = nd[0], c1 = nd[1];
+  const float c2 = nd[2].x;
+  const uint32_t e = __float_as_uint(c0.w);
+  const f32x2 sx = {qscale(e, 0), qscale(e, 0)}, sy = {qscale(e, 1), qscale(e, 1)}, sz = {qscale(e, 2), qscale(e, 2)};
+  const f32x2 Ox = {c0.x, c0.x}, Oy = {c0.y, c0.y}, Oz = {c0.z, c0.z};
+  const uint32_t w0 = __float_as_uint(c1.x), w1 = __float_as_uint(c1.y), w2 = __float_as_uint(c1.z);
+  auto b = [](uint32_t w, int k) { return (float)((w >> (8 * k)) & 255u); };
+  const f32x2 lox = Ox + f32x2{b(w0, 0), b(w1, 2)} * sx, loy = Oy + f32x2{b(w0, 1), b(w1, 3)} * sy,
+              loz = Oz + f32x2{b(w0, 2), b(w2, 0)} * sz;
+  const f32x2 hix = Ox + f32x2{b(w0, 3), b(w2, 1)} * sx, hiy = Oy + f32x2{b(w1, 0), b(w2, 2)} * sy,
+              hiz = Oz + f32x2{b(w1, 1), b(w2, 3)} * sz;
+  slabPair(lox, loy, loz, hix, hiy, hiz, o, inv, h);
+  h.lref = __float_as_int(c1.w);
+  h.rref = __float_as_int(c2);
+}
+// a node record: exact (4 float4) or the runtime tree's quantized one (3); the
+// record kind is a compile-time property of the traversal (FAST_QUANT)
+template <bool QUANT>
+__device__ __forceinline__ void visitAny(const float4* nd, V3 o, V3 inv, NodeHit& h) {
+  if (QUANT) visitNodeQ(nd, o, inv, h);
+  else visitNode(nd, o, inv, h);
+}
+template <bool QUANT>
+constexpr int nodeF4() { return QUANT ? 3 : 4; }
 
 // hitTriangle IS:251-301, accept/reject and distance only. With the stored unit
 // normal Ng = normalize(cross(p2-p1,p3-p1)) and w = dot(Ng,p1) (computed on the
@@ -185,7 +224,8 @@ __device__ __forceinline__ bool isLeafRef(int ref) { return ref < 0 && ref != RE
 //
 // TIES: *tie is set when a lane meets a triangle at exactly its current closest
 // t (the visiting order decides such ties; see refReachable).
-template <bool ANYHIT, bool CULL, bool COUNT, class StackType, bool LDSTOP = false, bool TIES = false>
+template <bool ANYHIT, bool CULL, bool COUNT, class StackType, bool LDSTOP = false, bool TIES = false,
+          bool QUANT = false>
 __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
                                         bool anyRT = false, const float4* top = nullptr, bool* tie = nullptr) {
   V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -203,9 +243,9 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
         if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
       }
       NodeHit nh;
-      const float4* nd = S.bvh + 4 * (size_t)ref;
-      if (LDSTOP && ref < S.nTop) nd = top + 4 * ref;
-      visitNode(nd, o, inv, nh);
+      const float4* nd = S.bvh + (size_t)nodeF4<QUANT>() * ref;
+      if (LDSTOP && ref < S.nTop) nd = top + nodeF4<QUANT>() * ref;
+      visitAny<QUANT>(nd, o, inv, nh);
       const int lref = nh.lref, rref = nh.rref;
       const float d1 = nh.d1, d2 = nh.d2, t0l = nh.t0l, t0r = nh.t0r;
       bool h1 = (lref != REF_NONE) && d1 > 0.0f;
@@ -356,7 +396,7 @@ struct PacketEntry {
   int pad;
   unsigned long long mask;
 };
-template <bool CULL>
+template <bool CULL, bool QUANT = false>
 __device__ __forceinline__ int tracePacket(const SceneView& S, V3 o, V3 d, bool valid, float& tOut, bool& tie,
                                            PacketEntry* pstack, Counters& C, const float4* top) {
   const int lane = __lane_id();
@@ -371,8 +411,8 @@ __device__ __forceinline__ int tracePacket(const SceneView& S, V3 o, V3 d, bool 
   while (true) {
     if (ref >= 0) {  // internal node: one scalar record for the wave
       NodeHit nh;
-      if (top && ref < S.nTop) visitNode(top + 4 * ref, o, inv, nh);  // LDS broadcast
-      else visitNode(S.bvh + 4 * (size_t)ref, o, inv, nh);
+      if (top && ref < S.nTop) visitAny<QUANT>(top + nodeF4<QUANT>() * ref, o, inv, nh);  // LDS broadcast
+      else visitAny<QUANT>(S.bvh + (size_t)nodeF4<QUANT>() * ref, o, inv, nh);
       nh.lref = __builtin_amdgcn_readfirstlane(nh.lref);
       nh.rref = __builtin_amdgcn_readfirstlane(nh.rref);
       const bool active = (mask >> lane) & 1ull;
