@@ -54,6 +54,9 @@ constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
 #define PT_QUANT_NODES 0  // 1: the runtime tree's node records quantized to 8 bits per plane (measured slower: DESIGN.md)
 #endif
 constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
+#ifndef PT_FUSED_SLABS
+#define PT_FUSED_SLABS 1  // the runtime tree's slab tests as packed FMAs (pt_trace.h visitNodeF)
+#endif
 #ifndef PT_ACCEL_LEAF
 #define PT_ACCEL_LEAF 4  // most triangles per leaf of the runtime's tree
 #endif

@@ -41,7 +41,7 @@ struct Tracer {
     if (!COUNT && S.fast) {
       bool tie = false;
       const SceneView F = fastView(S);
-      const int pos = traceRay<false, CULL, false, Stack, (LDS_NODES > 0), true, FAST_QUANT>(F, o, d, t, st, C, false, top, &tie);
+      const int pos = traceRay<false, CULL, false, Stack, (LDS_NODES > 0), true, FAST_KIND>(F, o, d, t, st, C, false, top, &tie);
       int tri = pos >= 0 ? S.fastTri[pos] : -1;
       if (tie || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
         C.rays--;  // the same ray, counted once
@@ -62,7 +62,7 @@ struct Tracer {
     float t;
     if (!COUNT && S.fast) {
       const SceneView F = fastView(S);
-      const int pos = traceRay<true, CULL, false, Stack, (LDS_NODES > 0), false, FAST_QUANT>(F, o, d, t, st, C, false, top);
+      const int pos = traceRay<true, CULL, false, Stack, (LDS_NODES > 0), false, FAST_KIND>(F, o, d, t, st, C, false, top);
       if (pos < 0) return false;
       if (refReachable(S, S.fastTri[pos], o, d, t)) return true;
       C.rays--;
@@ -255,7 +255,7 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
   bool tie;
   int tri;
   if (p.scene.fast) {  // through the runtime's tree, checked against the reference's
-    const int pos = tracePacket<CULL, FAST_QUANT>(fastView(p.scene), eye, dir, valid, t, tie, pstack, C, top);
+    const int pos = tracePacket<CULL, FAST_KIND>(fastView(p.scene), eye, dir, valid, t, tie, pstack, C, top);
     tri = pos >= 0 ? p.scene.fastTri[pos] : -1;
     if (valid && (tie || (tri >= 0 && !refReachable(p.scene, tri, eye, dir, t)))) {
       C.rays--;  // the same ray, counted once
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_W
   __shared__ float4 s_nodes[LDS_NODES * 4];
   {
     const float4* src = p.scene.fast ? p.scene.fbvh : p.scene.bvh;  // the tree traversed first
-    const int n = p.scene.fast ? p.scene.fnTop * nodeF4<FAST_QUANT>() : p.scene.nTop * 4;
+    const int n = p.scene.fast ? p.scene.fnTop * nodeF4<FAST_KIND>() : p.scene.nTop * 4;
     for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
   }
   __syncthreads();

@@ -126,15 +126,65 @@ __device__ __forceinline__ void visitNodeQ(const float4* nd, V3 o, V3 inv, NodeH
   h.lref = __float_as_int(c1.w);
   h.rref = __float_as_int(c2);
 }
-// a node record: exact (4 float4) or the runtime tree's quantized one (3); the
-// record kind is a compile-time property of the traversal (FAST_QUANT)
-template <bool QUANT>
-__device__ __forceinline__ void visitAny(const float4* nd, V3 o, V3 inv, NodeHit& h) {
-  if (QUANT) visitNodeQ(nd, o, inv, h);
+// The runtime tree's slab tests fused: (plane - o) * inv as fma(plane, inv,
+// -o * inv), one packed FMA per axis and child pair instead of a subtract and a
+// multiply. The rounding differs from hitAABB's by about |o| * 2^-23 along each
+// axis, far inside the widening of the runtime tree's boxes (pt_runtime.cpp
+// uploadAccel), so the walk still meets every triangle the ray hits; results
+// found through it are checked against the reference tree as before. Never
+// used on the reference tree, whose d must be hitAABB's bit for bit.
+__device__ __forceinline__ void visitNodeF(const float4* nd, V3 inv, V3 noi, NodeHit& h) {
+  const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+  const f32x2 lox = {q0.x, q0.y}, loy = {q0.z, q0.w}, loz = {q1.x, q1.y};
+  const f32x2 hix = {q1.z, q1.w}, hiy = {q2.x, q2.y}, hiz = {q2.z, q2.w};
+  const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+  const f32x2 ox = {noi.x, noi.x}, oy = {noi.y, noi.y}, oz = {noi.z, noi.z};
+  const f32x2 fx = __builtin_elementwise_fma(hix, ix, ox), fy = __builtin_elementwise_fma(hiy, iy, oy),
+              fz = __builtin_elementwise_fma(hiz, iz, oz);
+  const f32x2 nx = __builtin_elementwise_fma(lox, ix, ox), ny = __builtin_elementwise_fma(loy, iy, oy),
+              nz = __builtin_elementwise_fma(loz, iz, oz);
+  float t1 = fminf(fmaxf(fx.x, nx.x), fminf(fmaxf(fy.x, ny.x), fmaxf(fz.x, nz.x)));
+  float t0 = fmaxf(fminf(fx.x, nx.x), fmaxf(fminf(fy.x, ny.x), fminf(fz.x, nz.x)));
+  h.t0l = t0;
+  h.d1 = (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
+  t1 = fminf(fmaxf(fx.y, nx.y), fminf(fmaxf(fy.y, ny.y), fmaxf(fz.y, nz.y)));
+  t0 = fmaxf(fminf(fx.y, nx.y), fmaxf(fminf(fy.y, ny.y), fminf(fz.y, nz.y)));
+  h.t0r = t0;
+  h.d2 = (t1 >= t0) ? ((t0 > 0.0f) ? t0 : t1) : -1.0f;
+  h.lref = __float_as_int(q3.x);
+  h.rref = __float_as_int(q3.y);
+}
+// The fused walk's per-ray constants: 1/d clamped to +-2^64 (a direction
+// component of 0 or near it would make plane * inv - o * inv an inf - inf NaN
+// or an overflow), and -o * inv. With the clamp, an axis the ray runs
+// (nearly) parallel to still gives a slab interval of the right sign that spans
+// at least +-2^64 x the origin's distance from the planes -- every t of
+// interest when the origin is inside, none when it is outside -- so the test
+// stays conservative there too.
+struct FusedRay {
+  V3 inv, noi;
+};
+__device__ __forceinline__ float clampInv(float v) { return copysignf(fminf(fabsf(v), 0x1p64f), v); }
+__device__ __forceinline__ FusedRay fusedRay(V3 o, V3 inv) {
+  FusedRay f;
+  f.inv = v3(clampInv(inv.x), clampInv(inv.y), clampInv(inv.z));
+  f.noi = v3(-(o.x * f.inv.x), -(o.y * f.inv.y), -(o.z * f.inv.z));
+  return f;
+}
+// Node kinds, a compile-time property of a traversal: the reference tree's
+// exact records and slab tests (NODE_EXACT), the runtime tree's quantized
+// records (NODE_QUANT, PT_QUANT_NODES) or its exact records with fused slab
+// tests (NODE_FUSED).
+constexpr int NODE_EXACT = 0, NODE_QUANT = 1, NODE_FUSED = 2;
+constexpr int FAST_KIND = FAST_QUANT ? NODE_QUANT : (PT_FUSED_SLABS ? NODE_FUSED : NODE_EXACT);
+template <int KIND>
+__device__ __forceinline__ void visitAny(const float4* nd, V3 o, V3 inv, const FusedRay& fr, NodeHit& h) {
+  if (KIND == NODE_QUANT) visitNodeQ(nd, o, inv, h);
+  else if (KIND == NODE_FUSED) visitNodeF(nd, fr.inv, fr.noi, h);
   else visitNode(nd, o, inv, h);
 }
-template <bool QUANT>
-constexpr int nodeF4() { return QUANT ? 3 : 4; }
+template <int KIND>
+constexpr int nodeF4() { return KIND == NODE_QUANT ? 3 : 4; }
 
 // hitTriangle IS:251-301, accept/reject and distance only. With the stored unit
 // normal Ng = normalize(cross(p2-p1,p3-p1)) and w = dot(Ng,p1) (computed on the
@@ -225,10 +275,11 @@ __device__ __forceinline__ bool isLeafRef(int ref) { return ref < 0 && ref != RE
 // TIES: *tie is set when a lane meets a triangle at exactly its current closest
 // t (the visiting order decides such ties; see refReachable).
 template <bool ANYHIT, bool CULL, bool COUNT, class StackType, bool LDSTOP = false, bool TIES = false,
-          bool QUANT = false>
+          int KIND = NODE_EXACT>
 __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
                                         bool anyRT = false, const float4* top = nullptr, bool* tie = nullptr) {
   V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const FusedRay fr = fusedRay(o, inv);  // NODE_FUSED
   float tbest = PT_INF;
   int best = -1;
   int ref = S.rootRef;   // next item in visiting order (REF_NONE only when the stack is empty too)
@@ -243,9 +294,9 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
         if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
       }
       NodeHit nh;
-      const float4* nd = S.bvh + (size_t)nodeF4<QUANT>() * ref;
-      if (LDSTOP && ref < S.nTop) nd = top + nodeF4<QUANT>() * ref;
-      visitAny<QUANT>(nd, o, inv, nh);
+      const float4* nd = S.bvh + (size_t)nodeF4<KIND>() * ref;
+      if (LDSTOP && ref < S.nTop) nd = top + nodeF4<KIND>() * ref;
+      visitAny<KIND>(nd, o, inv, fr, nh);
       const int lref = nh.lref, rref = nh.rref;
       const float d1 = nh.d1, d2 = nh.d2, t0l = nh.t0l, t0r = nh.t0r;
       bool h1 = (lref != REF_NONE) && d1 > 0.0f;
@@ -396,11 +447,12 @@ struct PacketEntry {
   int pad;
   unsigned long long mask;
 };
-template <bool CULL, bool QUANT = false>
+template <bool CULL, int KIND = NODE_EXACT>
 __device__ __forceinline__ int tracePacket(const SceneView& S, V3 o, V3 d, bool valid, float& tOut, bool& tie,
                                            PacketEntry* pstack, Counters& C, const float4* top) {
   const int lane = __lane_id();
   const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const FusedRay fr = fusedRay(o, inv);  // NODE_FUSED
   float tbest = PT_INF;
   int best = -1;
   tie = false;
@@ -411,8 +463,8 @@ __device__ __forceinline__ int tracePacket(const SceneView& S, V3 o, V3 d, bool 
   while (true) {
     if (ref >= 0) {  // internal node: one scalar record for the wave
       NodeHit nh;
-      if (top && ref < S.nTop) visitAny<QUANT>(top + nodeF4<QUANT>() * ref, o, inv, nh);  // LDS broadcast
-      else visitAny<QUANT>(S.bvh + (size_t)nodeF4<QUANT>() * ref, o, inv, nh);
+      if (top && ref < S.nTop) visitAny<KIND>(top + nodeF4<KIND>() * ref, o, inv, fr, nh);  // LDS broadcast
+      else visitAny<KIND>(S.bvh + (size_t)nodeF4<KIND>() * ref, o, inv, fr, nh);
       nh.lref = __builtin_amdgcn_readfirstlane(nh.lref);
       nh.rref = __builtin_amdgcn_readfirstlane(nh.rref);
       const bool active = (mask >> lane) & 1ull;
