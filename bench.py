@@ -199,6 +199,7 @@ def main():
                        # the tree the timed frames traversed: the uploaded one, or the runtime's own
                        # binned-SAH tree with every result checked against the uploaded one
                        "traversal_tree": "runtime (checked against uploaded)" if st.runtime_tree else "uploaded",
+                       "waves_per_simd": st.waves_per_simd,
                        "parallelism": (f"screen-tile x{n}" + (" + RCCL gather per frame" if n > 1 else ""))
                        if args.shard == "tiles" else
                        (f"sample-parallel x{n}" + (" (RCCL reduce of the running means after the run)"

@@ -85,6 +85,8 @@ typedef struct pt_frame_stats {
                            long-path tiles (0 = one item per tile) */
   int runtime_tree;     /* megakernel: 1 when the last frame traversed the runtime's own tree
                            (results checked against the uploaded one), 0 the uploaded tree */
+  int waves_per_simd;   /* megakernel: waves per SIMD the last frame's kernel was compiled for
+                           (3 = the large-scene Disney/MIS variant, else its default bound) */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;

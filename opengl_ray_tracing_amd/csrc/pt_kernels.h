@@ -13,6 +13,14 @@ constexpr int BLOCK = 256;        // 4 waves of 64
 #ifndef PT_MIN_WAVES_LAMBERT
 #define PT_MIN_WAVES_LAMBERT 3    // Lambert megakernel: keep 3 waves/SIMD (<= 168 VGPRs, no spills)
 #endif
+// Scenes whose geometry outgrows the L2s by far (> PT_WIDE_SCENE_MB of records)
+// walk memory-latency bound: their Disney/MIS megakernels run the variant
+// compiled for WIDE_WAVES waves per SIMD (some VGPRs spilled), which keeps more
+// node fetches in flight (c5: 13.4 -> 10.5 ms; c3/c4, L2-resident: 1-5 % slower).
+#ifndef PT_WIDE_SCENE_MB
+#define PT_WIDE_SCENE_MB 64
+#endif
+constexpr int WIDE_WAVES = 3;
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
@@ -165,7 +173,8 @@ struct PackParams {
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);
 // hdr[k].w = cache[k].z, samp[k] = cache[k].xy (the Env render layout)
 hipError_t launchEnvPack(float4* hdr, const float4* cache, float2* samp, int n, hipStream_t s);
-hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count);
+hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count,
+                        bool wide = false);
 // tile order of the next frame: each queue band's groups of `group` consecutive
 // tiles sorted by this frame's summed cost, descending (tiles inside a group keep
 // their order, which keeps neighbouring tiles together for the caches)
@@ -174,7 +183,7 @@ constexpr int REORDER_MAX = 4096;  // most groups per band the one-block LDS sor
 // and zeroed; splitLg (one per tile) is the split state carried from frame to frame
 hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* order, int perQueue, int orderCap,
                          int numItems, int group, int numWaves, int splitPct, hipStream_t s);
-hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, int* nb);
+hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, bool wide, int* nb);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull);
 hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb);
 int regenLdsStack();

@@ -568,8 +568,11 @@ __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
   return v;
 }
 
-template <int INTEG, bool CULL, bool COUNT>
-__global__ __launch_bounds__(BLOCK, INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_WAVES) void renderKernel(RenderParams p) {
+// WAVES > 0: compiled for that many waves per SIMD (the latency-bound large
+// scenes' variant, pt_runtime.cpp renderFrame)
+template <int INTEG, bool CULL, bool COUNT, int WAVES = 0>
+__global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_WAVES)) void renderKernel(
+    RenderParams p) {
   __shared__ int s_stack[LDS_STACK * BLOCK];
   Stack st;
   st.lds = s_stack + threadIdx.x;
@@ -762,9 +765,11 @@ __global__ void fmathKernel(int fn, const float* x, const float* y, int n, float
 namespace pt {
 
 template <int I>
-static hipError_t launchRenderI(const RenderParams& p, int grid, hipStream_t s, bool cull, bool count) {
+static hipError_t launchRenderI(const RenderParams& p, int grid, hipStream_t s, bool cull, bool count, bool wide) {
   if (count) {
     hipLaunchKernelGGL((renderKernel<I, false, true>), dim3(grid), dim3(BLOCK), 0, s, p);
+  } else if (cull && wide && I != 0) {
+    hipLaunchKernelGGL((renderKernel<I, true, false, WIDE_WAVES>), dim3(grid), dim3(BLOCK), 0, s, p);
   } else if (cull) {
     hipLaunchKernelGGL((renderKernel<I, true, false>), dim3(grid), dim3(BLOCK), 0, s, p);
   } else {
@@ -773,19 +778,22 @@ static hipError_t launchRenderI(const RenderParams& p, int grid, hipStream_t s, 
   return hipGetLastError();
 }
 
-hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count) {
+hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count,
+                        bool wide) {
   switch (integrator) {
-    case 0: return launchRenderI<0>(p, grid, s, cull, count);
-    case 1: return launchRenderI<1>(p, grid, s, cull, count);
-    default: return launchRenderI<2>(p, grid, s, cull, count);
+    case 0: return launchRenderI<0>(p, grid, s, cull, count, wide);
+    case 1: return launchRenderI<1>(p, grid, s, cull, count, wide);
+    default: return launchRenderI<2>(p, grid, s, cull, count, wide);
   }
 }
 
-hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, int* nb) {
+hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, bool wide, int* nb) {
   const void* f;
 #define PT_SEL(I)                                                                              \
   f = count ? (const void*)renderKernel<I, false, true>                                        \
-            : (cull ? (const void*)renderKernel<I, true, false> : (const void*)renderKernel<I, false, false>)
+            : (cull ? (wide && I != 0 ? (const void*)renderKernel<I, true, false, WIDE_WAVES>   \
+                                      : (const void*)renderKernel<I, true, false>)             \
+                    : (const void*)renderKernel<I, false, false>)
   if (integrator == 0) { PT_SEL(0); }
   else if (integrator == 1) { PT_SEL(1); }
   else { PT_SEL(2); }

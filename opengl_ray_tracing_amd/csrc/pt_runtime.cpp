@@ -71,6 +71,7 @@ struct pt_ctx {
   int* d_cost = nullptr;   // per-tile cost of the last frame (megakernel)
   int* d_order = nullptr;  // per-band tile order for the next frame
   bool lastFast = false;    // the last megakernel frame traversed the runtime's tree
+  int lastWaves = 0;        // waves per SIMD of the last megakernel launch (occupancy query)
   // tree / tile-split policy probe (probePolicy): frames since the probe (re)started,
   // the summed frame times of each policy, the decision
   int probeFrame = 0;
@@ -915,8 +916,12 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   const bool regen = !count && (c.flags & PT_FLAG_REGEN);
   int nb = 0;
   if (regen) CK(regenBlocksPerCU(c.integrator, cull, &nb));
-  else CK(renderBlocksPerCU(c.integrator, cull, count, &nb));
+  // large scenes: the more-waves variant (pt_kernels.h PT_WIDE_SCENE_MB)
+  const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + 144) + (size_t)ctx->nDevNodes * 64;
+  const bool wide = !regen && !count && cull && c.integrator != 0 && sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
+  if (!regen) CK(renderBlocksPerCU(c.integrator, cull, count, wide, &nb));
   if (nb < 1) nb = 1;
+  ctx->lastWaves = regen ? 0 : nb * BLOCK / 64 / 4;  // 4 SIMDs per CU
   int grid = ctx->numCU * nb;
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK);
@@ -991,7 +996,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
 #endif
   CK(hipEventRecord(evb, ctx->stream));
   if (regen) CK(launchRegen(p, c.integrator, grid, ctx->stream, cull));
-  else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count));
+  else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count, wide));
 #if PT_WAVE_TRACE
   if (dTrace) {
     std::vector<unsigned long long> tr(nTrace);
@@ -1178,6 +1183,7 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   st->max_stack = ctx->maxStack;
   st->split_items = 0;
   st->runtime_tree = ctx->lastFast ? 1 : 0;
+  st->waves_per_simd = ctx->lastWaves;
   if (ctx->d_order && ctx->orderValid) {
     int counts[NUM_QUEUES];
     CK(hipMemcpy(counts, ctx->d_order + (size_t)NUM_QUEUES * ctx->orderCap, sizeof(counts), hipMemcpyDeviceToHost));

@@ -47,6 +47,7 @@ class FrameStats:
     max_stack: int
     split_items: int
     runtime_tree: int
+    waves_per_simd: int
 
 
 def _fp(a: np.ndarray):
@@ -195,7 +196,8 @@ class Renderer:
         s = _native.PtFrameStats()
         self._ck(self._lib.pt_get_stats(self._h, C.byref(s)), "pt_get_stats")
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
-                          s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree)
+                          s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
+                          s.waves_per_simd)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

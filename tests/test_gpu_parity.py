@@ -207,3 +207,28 @@ def test_tile_order_does_not_change_the_image(c4):
     b, sb = render_gpu(cfg, tris, nodes, hdr, frames=3, flags=FLAG_NO_TILE_ORDER)
     assert np.array_equal(a, b)
     assert sa.rays == sb.rays
+
+
+def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
+    """A scene past PT_WIDE_SCENE_MB (216k triangles here, like c5's heightfield + teapot)
+    runs the MIS megakernel compiled for 3 waves/SIMD; its pixels meet the oracle's under the
+    same tolerance as test_render_parity, and the runtime tree gives the uploaded tree's image."""
+    from opengl_ray_tracing_amd import FLAG_REFERENCE_TREE
+    s = scenes.scene_c3()
+    v, i = scenes.heightfield(330)
+    s.add_mesh(v, i, scenes.Material(baseColor=(0.6, 0.6, 0.65), roughness=0.4, metallic=0.2, specular=0.5),
+               scenes.get_transform_matrix((0, 0, 0), (0, -1.2, 0), (13.0, 13.0, 13.0)), True)
+    s.build_bvh("binned", 8)
+    tris, nodes = s.encode()
+    assert tris.size // 36 > 210000
+    cfg = scenes.CONFIGS["c5"]
+    hdr = scenes.load_hdr(scenes.HDR_FILES[cfg.env])
+    w, h, mb = 160, 90, 4
+    g, st = render_gpu(cfg, tris, nodes, hdr, frames=2, max_bounce=mb, w=w, h=h)
+    assert st.waves_per_simd == 3
+    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=2, max_bounce=mb, w=w, h=h, flags=FLAG_REFERENCE_TREE)
+    assert np.array_equal(g, b) and st.rays == sb.rays
+    px = parity.sample_pixels(w, h, w * h, seed=3)
+    o, _ = render_oracle(cfg, tris, nodes, hdr, px, frames=2, max_bounce=mb, w=w, h=h)
+    parity.assert_parity(g[px[:, 1], px[:, 0]], o[px[:, 1], px[:, 0]], "wide/mis")
+    assert np.all(g[..., 3] == 1.0)

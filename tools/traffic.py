@@ -11,6 +11,7 @@ Merges {config: {...}} into out.json (read by bench.py --traffic).
 import csv
 import glob
 import json
+import re
 import sys
 from pathlib import Path
 
@@ -27,8 +28,9 @@ def per_launch(d, counter, kernel_pat):
 def main():
     d, cfg, out = sys.argv[1], sys.argv[2], Path(sys.argv[3])
     pat = "renderKernel<"
-    fe = [v for k, v in per_launch(f"{d}/fetch", "FETCH_SIZE", pat) if k.endswith("true, false>(pt::RenderParams)")]
-    wr = [v for k, v in per_launch(f"{d}/write", "WRITE_SIZE", pat) if k.endswith("true, false>(pt::RenderParams)")]
+    bench = re.compile(r"true, false(, \d+)?>\(pt::RenderParams\)$")  # the culling frame kernel (any waves variant)
+    fe = [v for k, v in per_launch(f"{d}/fetch", "FETCH_SIZE", pat) if bench.search(k)]
+    wr = [v for k, v in per_launch(f"{d}/write", "WRITE_SIZE", pat) if bench.search(k)]
     if not fe or not wr:
         raise SystemExit("no bench-kernel dispatches found")
     f_kb, w_kb = sum(fe) / len(fe), sum(wr) / len(wr)
