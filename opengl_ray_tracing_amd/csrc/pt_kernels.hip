@@ -441,14 +441,25 @@ __global__ __launch_bounds__(BLOCK) void basicKernel(BasicParams p) {
 //    splitPct % of a wave's share of the band (band cost / waves per band)
 //    is split once more (2^lg items of 64 >> lg pixels, lg <= 6); one whose
 //    items became cheap (< 1/4 of that) is merged back one step.
-//  * Order: items sorted by their tile's longest item, descending (ties by tile
-//    id; bitonic in LDS), so the long ones start first. Progressive frames share
-//    camera and scene, so this frame's costs predict the next frame's.
+//  * Order: items by their tile's longest item, descending, so the long ones
+//    start first: a counting sort over 128 cost buckets (the cost's octave and
+//    two more bits, ~19 % wide; order within a bucket is arbitrary) -- one pass
+//    of LDS atomics instead of a bitonic sort's 55 barrier phases. Progressive
+//    frames share camera and scene, so this frame's costs predict the next's.
 // group > 1 sorts groups of consecutive tiles by summed cost and never splits.
+constexpr int REORDER_BUCKETS = 128;
+__device__ __forceinline__ int costBucket(unsigned long long c) {  // 0 = most expensive
+  const unsigned v = (unsigned)min(c, 0xffffffffull) | 1u;
+  const int oct = 31 - __clz(v);
+  const int frac = oct >= 2 ? (int)((v >> (oct - 2)) & 3u) : (int)((v << (2 - oct)) & 3u);
+  return REORDER_BUCKETS - 1 - (oct * 4 + frac);
+}
 __global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, int* splitLg, int* order, int perQueue,
                                                        int orderCap, int numItems, int group, int numWaves,
                                                        int splitPct) {
-  __shared__ unsigned long long key[REORDER_MAX];
+  __shared__ int bucketOf[REORDER_MAX];  // each group's bucket
+  __shared__ int rankG[REORDER_MAX];     // the group at each rank, most expensive first
+  __shared__ int start[REORDER_BUCKETS];
   __shared__ int scan[1024];
   __shared__ int partialPos;
   __shared__ unsigned long long sumCost;
@@ -458,9 +469,8 @@ __global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, i
   const int ng = (n + group - 1) / group;  // groups of `group` consecutive tiles (the last may be short)
   const int lastSize = n - (ng - 1) * group;
   const bool splitting = group == 1 && splitLg != nullptr && splitPct > 0;
-  int size = 1;
-  while (size < ng) size <<= 1;
   if (threadIdx.x == 0) sumCost = 0;
+  if (threadIdx.x < REORDER_BUCKETS) start[threadIdx.x] = 0;
   __syncthreads();
   unsigned long long mySum = 0;
   for (int g = threadIdx.x; g < ng; g += blockDim.x) {
@@ -472,54 +482,51 @@ __global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, i
   // a wave's share of the band's work: the cost above which an item forms the tail
   const unsigned long long share = sumCost / (unsigned long long)max(1, numWaves / NUM_QUEUES);
   const unsigned long long target = max(share * (unsigned long long)splitPct / 100ull, 1ull);
-  for (int g = threadIdx.x; g < size; g += blockDim.x) {
-    unsigned long long k = 0;  // padding sorts last
-    if (g < ng) {
-      unsigned long long c = 0;
-      const int t0 = base + g * group, t1 = min(t0 + group, base + n);
-      if (splitting) {
-        const int t = t0;
-        const unsigned long long m = (unsigned)max(costMax[t], 1);
-        int lg = splitLg[t];
-        if (m > target && lg < MAX_SPLIT_LG) lg++;
-        else if (lg > 0 && 4 * m < target) lg--;
-        splitLg[t] = lg;
-        c = m;
-        costMax[t] = 0;
-      } else {
-        for (int t = t0; t < t1; t++) c += (unsigned)max(cost[t], 1);
-        if (costMax)
-          for (int t = t0; t < t1; t++) costMax[t] = 0;
-      }
-      for (int t = t0; t < t1; t++) cost[t] = 0;
-      k = (min(c, 0xffffffffull) << 32) | (unsigned)(0x7fffffff - g);
+  for (int g = threadIdx.x; g < ng; g += blockDim.x) {
+    unsigned long long c = 0;
+    const int t0 = base + g * group, t1 = min(t0 + group, base + n);
+    if (splitting) {
+      const int t = t0;
+      const unsigned long long m = (unsigned)max(costMax[t], 1);
+      int lg = splitLg[t];
+      if (m > target && lg < MAX_SPLIT_LG) lg++;
+      else if (lg > 0 && 4 * m < target) lg--;
+      splitLg[t] = lg;
+      c = m;
+      costMax[t] = 0;
+    } else {
+      for (int t = t0; t < t1; t++) c += (unsigned)max(cost[t], 1);
+      if (costMax)
+        for (int t = t0; t < t1; t++) costMax[t] = 0;
     }
-    key[g] = k;
+    for (int t = t0; t < t1; t++) cost[t] = 0;
+    const int bk = costBucket(c);
+    bucketOf[g] = bk;
+    atomicAdd(&start[bk], 1);
   }
   __syncthreads();
-  for (int k = 2; k <= size; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < size; i += blockDim.x) {
-        const int l = i ^ j;
-        if (l > i) {
-          const bool desc = (i & k) == 0;  // descending overall
-          const unsigned long long a = key[i], b = key[l];
-          if (desc ? (a < b) : (a > b)) {
-            key[i] = b;
-            key[l] = a;
-          }
-        }
-      }
-      __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the bucket counts, one wave
+    const int lane = threadIdx.x;
+    const int c0 = start[2 * lane], c1 = start[2 * lane + 1];
+    int incl = c0 + c1;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
     }
+    const int excl = incl - c0 - c1;
+    start[2 * lane] = excl;
+    start[2 * lane + 1] = excl + c0;
   }
+  __syncthreads();
+  for (int g = threadIdx.x; g < ng; g += blockDim.x) rankG[atomicAdd(&start[bucketOf[g]], 1)] = g;
+  __syncthreads();
   int* out = order + (size_t)q * orderCap;
   if (splitting) {
-    // item offsets: exclusive scan of 2^lg over the sorted ranks (4 ranks per thread)
+    // item offsets: exclusive scan of 2^lg over the ranks (ceil(ng / 1024) ranks per thread)
     const int per = (ng + 1023) / 1024;
     const int r0 = min(ng, (int)threadIdx.x * per), r1 = min(ng, r0 + per);
     int local = 0;
-    for (int r = r0; r < r1; r++) local += 1 << splitLg[base + 0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu)];
+    for (int r = r0; r < r1; r++) local += 1 << splitLg[base + rankG[r]];
     scan[threadIdx.x] = local;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
@@ -532,7 +539,7 @@ __global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, i
     if (total <= orderCap) {
       int pos = scan[threadIdx.x] - local;
       for (int r = r0; r < r1; r++) {
-        const int t = base + 0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu);
+        const int t = base + rankG[r];
         const int lg = splitLg[t];
         for (int sIdx = 0; sIdx < (1 << lg); sIdx++) out[pos++] = t | sIdx << ITEM_TILE_BITS | lg << 28;
       }
@@ -543,10 +550,10 @@ __global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, i
     for (int r = threadIdx.x; r < ng; r += blockDim.x) splitLg[base + r] = 0;
   }
   for (int r = threadIdx.x; r < ng; r += blockDim.x)
-    if (0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu) == ng - 1) partialPos = r;
+    if (rankG[r] == ng - 1) partialPos = r;
   __syncthreads();
   for (int r = threadIdx.x; r < ng; r += blockDim.x) {
-    const int g = 0x7fffffff - (int)(unsigned)(key[r] & 0xffffffffu);
+    const int g = rankG[r];
     const int off = r * group - (r > partialPos ? group - lastSize : 0);
     const int len = g == ng - 1 ? lastSize : group;
     for (int k = 0; k < len; k++) out[off + k] = base + g * group + k;
