@@ -1011,12 +1011,12 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
     }
   }
 #endif
+  CK(hipEventRecord(eve, ctx->stream));  // kernel_ms: the frame kernel alone (the reorder below is in the frame's wall time)
   if (ordered) {
     CK(launchReorder(ctx->d_cost, ctx->d_cost + ctx->numItems, ctx->d_cost + 2 * (size_t)ctx->numItems, ctx->d_order,
                      ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, ctx->stream));
     ctx->orderValid = true;
   }
-  CK(hipEventRecord(eve, ctx->stream));
   ctx->launches++;
   return PT_OK;
 }
