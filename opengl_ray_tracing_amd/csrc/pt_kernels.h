@@ -17,6 +17,9 @@ constexpr int BLOCK = 256;        // 4 waves of 64
 // walk memory-latency bound: their Disney/MIS megakernels run the variant
 // compiled for WIDE_WAVES waves per SIMD (some VGPRs spilled), which keeps more
 // node fetches in flight (c5: 13.4 -> 10.5 ms; c3/c4, L2-resident: 1-5 % slower).
+#ifndef PT_COST_EMA
+#define PT_COST_EMA 2  // order tiles by a running estimate of their cost, this frame's weighted 2^-PT_COST_EMA (0 = off)
+#endif
 #ifndef PT_WIDE_SCENE_MB
 #define PT_WIDE_SCENE_MB 64
 #endif
@@ -181,7 +184,7 @@ hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStre
 constexpr int REORDER_MAX = 4096;  // most groups per band the one-block LDS sort handles
 // order: NUM_QUEUES * orderCap items, then NUM_QUEUES item counts; cost / costMax are read
 // and zeroed; splitLg (one per tile) is the split state carried from frame to frame
-hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* order, int perQueue, int orderCap,
+hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* ema, int* order, int perQueue, int orderCap,
                          int numItems, int group, int numWaves, int splitPct, hipStream_t s);
 hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, bool wide, int* nb);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull);

@@ -454,7 +454,8 @@ __device__ __forceinline__ int costBucket(unsigned long long c) {  // 0 = most e
   const int frac = oct >= 2 ? (int)((v >> (oct - 2)) & 3u) : (int)((v << (2 - oct)) & 3u);
   return REORDER_BUCKETS - 1 - (oct * 4 + frac);
 }
-__global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, int* splitLg, int* order, int perQueue,
+__global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, int* splitLg, int* ema, int* order,
+                                                       int perQueue,
                                                        int orderCap, int numItems, int group, int numWaves,
                                                        int splitPct) {
   __shared__ int bucketOf[REORDER_MAX];  // each group's bucket
@@ -500,6 +501,12 @@ __global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, i
         for (int t = t0; t < t1; t++) costMax[t] = 0;
     }
     for (int t = t0; t < t1; t++) cost[t] = 0;
+    if constexpr (PT_COST_EMA > 0) {  // a path's cost varies frame to frame: rank by the running estimate
+      const unsigned long long e = (unsigned)ema[base + g];
+      constexpr int S = PT_COST_EMA > 0 ? PT_COST_EMA : 1;  // weight of this frame: 2^-S
+      c = e ? (((1ull << S) - 1) * e + min(c, 0x7fffffffull) + (1ull << (S - 1))) >> S : min(c, 0x7fffffffull);
+      ema[base + g] = (int)c;
+    }
     const int bk = costBucket(c);
     bucketOf[g] = bk;
     atomicAdd(&start[bk], 1);
@@ -561,10 +568,10 @@ __global__ __launch_bounds__(1024) void reorderKernel(int* cost, int* costMax, i
   if (threadIdx.x == 0) order[(size_t)NUM_QUEUES * orderCap + q] = n;
 }
 
-hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* order, int perQueue, int orderCap,
+hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* ema, int* order, int perQueue, int orderCap,
                          int numItems, int group, int numWaves, int splitPct, hipStream_t s) {
   if ((perQueue + group - 1) / group > REORDER_MAX || orderCap < perQueue) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(reorderKernel, dim3(NUM_QUEUES), dim3(1024), 0, s, cost, costMax, splitLg, order, perQueue,
+  hipLaunchKernelGGL(reorderKernel, dim3(NUM_QUEUES), dim3(1024), 0, s, cost, costMax, splitLg, ema, order, perQueue,
                      orderCap, numItems, group, numWaves, splitPct);
   return hipGetLastError();
 }

@@ -853,8 +853,9 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
     ctx->probeN[0] = ctx->probeN[1] = ctx->probeN[2] = 0;
     ctx->probeMs[0] = ctx->probeMs[1] = ctx->probeMs[2] = 0.0;
     ctx->treeDecided = ctx->splitDecided = -1;
-    if (ctx->d_cost) (void)hipMemsetAsync(ctx->d_cost + 2 * (size_t)ctx->numItems, 0, (size_t)ctx->numItems * sizeof(int),
-                                          ctx->stream);
+    // split state and cost estimates start over (the camera or scene changed)
+    if (ctx->d_cost) (void)hipMemsetAsync(ctx->d_cost + 2 * (size_t)ctx->numItems, 0,
+                                          2 * (size_t)ctx->numItems * sizeof(int), ctx->stream);
   }
   const int f = ctx->probeFrame < 1000 ? ctx->probeFrame++ : 1000;
   // the previous frame's time (its launch is the last recorded one) into its probe slot
@@ -964,8 +965,8 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   ctx->orderCap = orderCap;
   if (ordered && !ctx->d_cost) {
     // per tile: summed item cost, longest item, split state (reorderKernel reads and zeroes the costs)
-    CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * 3 * sizeof(int)));
-    CK(hipMemsetAsync(ctx->d_cost, 0, (size_t)ctx->numItems * 3 * sizeof(int), ctx->stream));
+    CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * 4 * sizeof(int)));
+    CK(hipMemsetAsync(ctx->d_cost, 0, (size_t)ctx->numItems * 4 * sizeof(int), ctx->stream));
     // per band: orderCap work items, then the NUM_QUEUES item counts (reorderKernel)
     CK(hipMalloc(&ctx->d_order, ((size_t)NUM_QUEUES * orderCap + NUM_QUEUES) * sizeof(int)));
     ctx->orderValid = false;
@@ -1013,7 +1014,8 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
 #endif
   CK(hipEventRecord(eve, ctx->stream));  // kernel_ms: the frame kernel alone (the reorder below is in the frame's wall time)
   if (ordered) {
-    CK(launchReorder(ctx->d_cost, ctx->d_cost + ctx->numItems, ctx->d_cost + 2 * (size_t)ctx->numItems, ctx->d_order,
+    CK(launchReorder(ctx->d_cost, ctx->d_cost + ctx->numItems, ctx->d_cost + 2 * (size_t)ctx->numItems,
+                     ctx->d_cost + 3 * (size_t)ctx->numItems, ctx->d_order,
                      ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, ctx->stream));
     ctx->orderValid = true;
   }
