@@ -140,3 +140,41 @@ class SampleReduce:
     def __call__(self):
         self.r.accum_into(self.img.data_ptr())
         return combine_sample_means(self.img, self.rank, self.world)
+
+
+def broadcast_scene(build, rank: int, device=None):
+    """Build the scene once on rank 0 and broadcast it to every rank.
+
+    The reference uploads its TBOs once from the one process it has
+    (OpenglRayTracing/main.cpp:720-735); with one process per GPU every rank
+    needs the same arrays, and running the host BVH build on all ranks at once
+    only makes them contend for the host cores. `build()` -> (tris, nodes, hdr)
+    runs on rank 0 alone; the arrays then travel as one broadcast each (device
+    tensors over RCCL/xGMI, host tensors under gloo) and come back as host
+    numpy arrays ready for Renderer.upload_scene / upload_env. Returns
+    (tris, nodes, hdr) on every rank, bit-identical to rank 0's; hdr may be None.
+    """
+    import torch
+    import torch.distributed as dist
+
+    arrays = build() if rank == 0 else (None, None, None)
+    shapes = [None if a is None else tuple(np.asarray(a).shape) for a in arrays]
+    obj = [shapes]
+    dist.broadcast_object_list(obj, src=0)
+    shapes = obj[0]
+    on_device = device is not None and not _staged()
+    out = []
+    for a, shp in zip(arrays, shapes):
+        if shp is None:
+            out.append(None)
+            continue
+        if rank == 0:
+            a = np.ascontiguousarray(a, np.float32)
+            t = torch.from_numpy(a)
+        else:
+            t = torch.empty(shp, dtype=torch.float32)
+        if on_device:
+            t = t.to(device)
+        dist.broadcast(t, src=0)
+        out.append(a if rank == 0 else t.cpu().numpy())
+    return tuple(out)

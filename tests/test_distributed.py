@@ -142,3 +142,40 @@ def test_gloo_sample_parallel_mean(world):
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def _bcast_worker(rank, world, port, q):
+    from opengl_ray_tracing_amd import scenes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def build():
+            s = scenes.scene_c2()
+            s.build_bvh("sah", 8)
+            tris, nodes = s.encode()
+            return tris, nodes, scenes.synthetic_env(64, 32)
+
+        tris, nodes, hdr = D.broadcast_scene(build, rank)
+        tris2, nodes2, none = D.broadcast_scene(lambda: (np.arange(72.0), np.ones(12), None), rank)
+        if rank != 0:  # every rank compares its arrays with a local build of the same scene
+            rt, rn, rh = build()
+            q.put(bool(np.array_equal(tris, rt) and np.array_equal(nodes, rn) and np.array_equal(hdr, rh)
+                       and tris.dtype == np.float32 and np.array_equal(tris2, np.arange(72.0))
+                       and nodes2.shape == (12,) and none is None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_broadcast_scene(world):
+    """The scene built on rank 0 arrives bit-identical on every other rank (hdr may be None)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert all(q.get(timeout=5) is True for _ in range(world - 1))
