@@ -7,13 +7,15 @@ running-mean accumulate. Default workload: configs[1] = c2, the
 OpenglRayTracing bunny scene (5k tris) at 1920x1080, Lambert, 2 bounces.
 
 N > 1 ranks (one process per GPU):
-  --shard samples (default, weak scaling): every rank renders the whole frame
-      from its own interleaved sample stream (rank r: samples r, r+N, ...), no
+  --shard tiles (default, strong scaling: BASELINE north_star's split): every
+      rank renders its 32x32 screen tiles of the one frame; every step presents
+      the frame on rank 0 by an RCCL gather of the packed shards (bit-exact
+      reassembly), pipelined one frame deep: frame f's gather runs on a
+      communication stream while frame f+1 renders.
+  --shard samples (weak scaling): every rank renders the whole frame from its
+      own interleaved sample stream (rank r: samples r, r+N, ...), no
       collective per step; the ranks' running means are combined by one RCCL
       reduce after the timed steps (validated, not timed).
-  --shard tiles (strong scaling): every rank renders its 32x32 screen tiles of
-      the one frame; each step ends with the RCCL gather of the packed shards
-      to rank 0 (bit-exact reassembly).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver launch for N > 1)
@@ -58,7 +60,7 @@ def parse():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="rehearsal: every rank on device 0")
-    ap.add_argument("--shard", choices=["samples", "tiles"], default="samples",
+    ap.add_argument("--shard", choices=["samples", "tiles"], default="tiles",
                     help="N > 1: sample-parallel full frames (weak) or screen-tile shards of one frame (strong)")
     return ap.parse_args()
 
@@ -147,6 +149,14 @@ def main():
     sync_all()
     t1 = time.perf_counter()
     st = r.stats()
+    # interactive cost after a camera reset (the reference zeroes frameCounter on every mouse
+    # move, OpenglRayTracing/main.cpp:611-634): frames 0..PROBE_FRAMES-1 of a restarted running
+    # mean, including the renderer's policy probe, timed like the steps
+    t2 = time.perf_counter()
+    for f in range(PROBE_FRAMES):
+        step(f)
+    sync_all()
+    reset_ms = 1e3 * (time.perf_counter() - t2) / PROBE_FRAMES
     combined_finite = None
     if combine is not None:  # the ranks' running means -> one image on rank 0 (after the timed steps)
         img = combine()
@@ -163,6 +173,9 @@ def main():
         sm = tt.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0].item())
+        rs = torch.tensor([reset_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(rs, op=dist.ReduceOp.MAX)
+        reset_ms = float(rs[0].item())
         rays_total = float(sm[1].item())
         kernel_ms_avg = float(mx[2].item()) / max(st.launches, 1)
     else:
@@ -189,6 +202,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "probe_frames": PROBE_FRAMES, "ms_per_step": round(ms_per_step, 4),
+            "reset_ms_per_frame": round(reset_ms, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.shard == "tiles" else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
@@ -251,11 +265,8 @@ def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, seconds):
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle  # noqa: E402  (bench.py's cpu_baseline leg is the only bench use of oracle/)
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    host = host_cpu()
+    cores = host["threads"]
     orc = oracle.Oracle(tris, nodes, hdr)
     acc = np.zeros((cfg.height, cfg.width, 4), np.float32)
     rays = 0
@@ -271,7 +282,30 @@ def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, seconds):
     dt = time.perf_counter() - t0
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"{frames} full {cfg.width}x{cfg.height} frames of {cfg.name} ({rays} rays, {dt:.1f} s)",
-            "ms_per_frame": round(1e3 * dt / frames, 1)}
+            "ms_per_frame": round(1e3 * dt / frames, 1), "host": host}
+
+
+def host_cpu():
+    """The host cores the CPU baseline may use: every CPU in this process's affinity mask,
+    bounded by the job's CPU share when the environment states one (OMP_NUM_THREADS: the GPU
+    box grants 16 cores per GPU and says so there; nproc shows the whole machine)."""
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    threads = min(affinity, int(share)) if share.isdigit() and int(share) > 0 else affinity
+    model = None
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"threads": max(1, threads), "nproc": nproc, "affinity": affinity,
+            "omp_num_threads": share or None, "cpu_model": model}
 
 
 if __name__ == "__main__":

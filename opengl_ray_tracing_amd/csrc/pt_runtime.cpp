@@ -24,6 +24,8 @@
 
 using namespace pt;
 
+static constexpr int EV_RING = 64;
+
 #ifndef PT_TILE_GROUP
 #define PT_TILE_GROUP 1  // tiles ordered by cost in groups of this many consecutive tiles (1 measured best)
 #endif
@@ -33,8 +35,19 @@ struct pt_ctx {
   pt_config cfg{};
   std::string err;
   hipStream_t own = nullptr, stream = nullptr;
-  std::vector<hipEvent_t> evs;  // begin/end pairs of the launches since the last reset
-  int launches = 0;
+  // Launch timing: a fixed ring of begin/end event pairs. Launch number i (since
+  // pt_create) records into pair i % EV_RING; a launch's elapsed time is folded
+  // into the running totals once its end event has completed (non-blocking on
+  // every new launch, blocking only when the ring is full or stats are read), so
+  // the cost per frame stays constant however long a caller renders.
+  hipEvent_t ev[2 * EV_RING] = {};
+  int evProbe[EV_RING] = {};    // probe slot of the launch in each ring position (-1 none)
+  int evGen[EV_RING] = {};      // probe generation it was tagged in
+  long long issued = 0, folded = 0;
+  double msTotal = 0.0;         // summed device time of the folded launches since the reset
+  float msLast = 0.0f;          // device time of the last folded launch
+  int launches = 0;             // render launches since the reset
+  int tagSlot = -1;             // probe slot for the launch being issued (probePolicy)
   int numCU = 0;
   // scene
   float4* d_geo = nullptr;
@@ -77,6 +90,8 @@ struct pt_ctx {
   int probeFrame = 0;
   int probeN[3] = {0, 0, 0};           // timed frames: runtime tree, uploaded tree (both unsplit), split
   double probeMs[3] = {0.0, 0.0, 0.0};
+  long long probeLast[3] = {-1, -1, -1};  // launch number of each slot's last timed frame
+  int probeGen = 0;
   int treeDecided = -1, splitDecided = -1;  // -1 probing, 0 off, 1 on
   int orderCap = 0;        // work items per band in d_order
   bool orderValid = false;
@@ -218,7 +233,8 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
   freeWavefront(ctx);
-  for (hipEvent_t e : ctx->evs) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -650,17 +666,55 @@ static int defaultBounce(int integ) {
   }
 }
 
-// begin/end events of launch number ctx->launches (created on first use)
-static int launchEvents(pt_ctx* ctx, hipEvent_t* b, hipEvent_t* e) {
-  size_t need = 2 * (size_t)(ctx->launches + 1);
-  while (ctx->evs.size() < need) {
-    hipEvent_t ev;
-    CK(hipEventCreate(&ev));
-    ctx->evs.push_back(ev);
+// Fold the oldest unfolded launch's device time into the totals (and into its
+// probe slot). blocking = false returns false instead of waiting for it.
+static bool foldOne(pt_ctx* ctx, bool blocking) {
+  if (ctx->folded >= ctx->issued) return false;
+  const int k = (int)(ctx->folded % EV_RING);
+  hipEvent_t b = ctx->ev[2 * k], e = ctx->ev[2 * k + 1];
+  if (blocking) (void)hipEventSynchronize(e);
+  else if (hipEventQuery(e) != hipSuccess) return false;
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, b, e) != hipSuccess) ms = 0.0f;
+  ctx->msTotal += ms;
+  ctx->msLast = ms;
+  const int slot = ctx->evProbe[k];
+  if (slot >= 0 && ctx->evGen[k] == ctx->probeGen) {
+    ctx->probeMs[slot] += ms;
+    ctx->probeN[slot]++;
   }
-  *b = ctx->evs[2 * ctx->launches];
-  *e = ctx->evs[2 * ctx->launches + 1];
+  ctx->folded++;
+  return true;
+}
+
+// fold every launch up to launch number `upto` (inclusive), waiting for them
+static void foldUpTo(pt_ctx* ctx, long long upto) {
+  while (ctx->folded <= upto && foldOne(ctx, true)) {
+  }
+}
+
+// begin/end events for the next launch (launch number ctx->issued)
+static int launchEvents(pt_ctx* ctx, hipEvent_t* b, hipEvent_t* e) {
+  while (foldOne(ctx, false)) {
+  }
+  if (ctx->issued - ctx->folded >= EV_RING) foldOne(ctx, true);
+  const int k = (int)(ctx->issued % EV_RING);
+  for (int j = 2 * k; j < 2 * k + 2; j++)
+    if (!ctx->ev[j]) CK(hipEventCreate(&ctx->ev[j]));
+  *b = ctx->ev[2 * k];
+  *e = ctx->ev[2 * k + 1];
   return PT_OK;
+}
+
+// the launch whose events launchEvents handed out has been enqueued
+static void commitLaunch(pt_ctx* ctx) {
+  const int k = (int)(ctx->issued % EV_RING);
+  ctx->evProbe[k] = ctx->tagSlot;
+  ctx->evGen[k] = ctx->probeGen;
+  if (ctx->tagSlot >= 0) ctx->probeLast[ctx->tagSlot] = ctx->issued;
+  ctx->tagSlot = -1;
+  ctx->issued++;
+  ctx->launches++;
 }
 
 // the RNG / Sobol sample index of frame frameCounter: sample-parallel ranks
@@ -824,7 +878,7 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
     CK(wfLaunchShade(p, c.integrator, s, gridShade, ctx->stream));
   }
   CK(hipEventRecord(eve, ctx->stream));
-  ctx->launches++;
+  commitLaunch(ctx);
   return PT_OK;
 }
 
@@ -840,43 +894,52 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
 //    issue cycles).
 // After a restart of the running mean (frameCounter 0, as on every camera move
 // in the reference): frames 1-2 run the runtime's tree and 3-4 the uploaded
-// one, unsplit; the faster tree is kept; frames 5-11 split (5-9 let the
-// per-tile split state converge, 10-11 are timed) and the faster split policy
-// is kept until the next restart. Sets *useFast; returns the split percentage
+// one, unsplit; frame 5 runs the runtime's tree while the host, at frame 6,
+// waits for frame 4 (frame 5 is already queued, so the GPU never drains) and
+// keeps the faster tree; frames 6-10 split (the per-tile split state
+// converges), 11-12 are timed, and at frame 14 -- waiting for frame 12 with 13
+// queued -- the faster split policy is kept until the next restart. No frame
+// waits for its own predecessor. Sets *useFast; returns the split percentage
 // for this frame's reorder (0 = off).
 static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast) {
   *useFast = fastAllowed;
+  ctx->tagSlot = -1;
   if (!ordered) return 0;
   if (!PT_SPLIT_AUTO) return PT_SPLIT_PCT;
   if (frameCounter == 0) {
+    ctx->probeGen++;
     ctx->probeFrame = 0;
-    ctx->probeN[0] = ctx->probeN[1] = ctx->probeN[2] = 0;
-    ctx->probeMs[0] = ctx->probeMs[1] = ctx->probeMs[2] = 0.0;
+    for (int k = 0; k < 3; k++) {
+      ctx->probeN[k] = 0;
+      ctx->probeMs[k] = 0.0;
+      ctx->probeLast[k] = -1;
+    }
     ctx->treeDecided = ctx->splitDecided = -1;
     // split state and cost estimates start over (the camera or scene changed)
     if (ctx->d_cost) (void)hipMemsetAsync(ctx->d_cost + 2 * (size_t)ctx->numItems, 0,
                                           2 * (size_t)ctx->numItems * sizeof(int), ctx->stream);
   }
   const int f = ctx->probeFrame < 1000 ? ctx->probeFrame++ : 1000;
-  // the previous frame's time (its launch is the last recorded one) into its probe slot
-  const int slot = (f == 2 || f == 3) ? 0 : (f == 4 || f == 5) ? 1 : (f == 11 || f == 12) ? 2 : -1;
-  if (slot >= 0 && ctx->launches > 0 && ctx->splitDecided < 0) {
-    float ms = 0.0f;
-    hipEvent_t b = ctx->evs[2 * (ctx->launches - 1)], e = ctx->evs[2 * (ctx->launches - 1) + 1];
-    if (hipEventSynchronize(e) == hipSuccess && hipEventElapsedTime(&ms, b, e) == hipSuccess) {
-      ctx->probeMs[slot] += ms;
-      ctx->probeN[slot]++;
-    }
-  }
   auto avg = [&](int k) { return ctx->probeN[k] ? ctx->probeMs[k] / ctx->probeN[k] : 1e30; };
-  if (f == 5 && ctx->treeDecided < 0) ctx->treeDecided = fastAllowed && avg(0) <= avg(1) ? 1 : 0;
-  if (f == 12 && ctx->splitDecided < 0) ctx->splitDecided = PT_SPLIT_PCT > 0 && avg(2) < avg(ctx->treeDecided ? 0 : 1) ? 1 : 0;
-  // this frame's tree
-  if (ctx->treeDecided >= 0) *useFast = fastAllowed && ctx->treeDecided;
-  else *useFast = fastAllowed && f <= 2;
+  if (f == 6 && ctx->treeDecided < 0) {
+    foldUpTo(ctx, std::max(ctx->probeLast[0], ctx->probeLast[1]));
+    ctx->treeDecided = fastAllowed && avg(0) <= avg(1) ? 1 : 0;
+  }
+  if (f == 14 && ctx->splitDecided < 0) {
+    foldUpTo(ctx, ctx->probeLast[2]);
+    ctx->splitDecided = PT_SPLIT_PCT > 0 && avg(2) < avg(ctx->treeDecided ? 0 : 1) ? 1 : 0;
+  }
+  // this frame's tree, and the probe slot its time goes to
+  if (ctx->treeDecided >= 0) {
+    *useFast = fastAllowed && ctx->treeDecided;
+  } else {
+    *useFast = fastAllowed && (f <= 2 || f == 5);
+    ctx->tagSlot = (f == 1 || f == 2) ? 0 : (f == 3 || f == 4) ? 1 : -1;
+  }
   // this frame's split policy (for the next frame's items)
   if (ctx->splitDecided >= 0) return ctx->splitDecided ? PT_SPLIT_PCT : 0;
-  return f >= 5 ? PT_SPLIT_PCT : 0;
+  if (f == 11 || f == 12) ctx->tagSlot = 2;
+  return f >= 6 ? PT_SPLIT_PCT : 0;
 }
 
 int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
@@ -904,7 +967,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
     CK(hipEventRecord(evb, ctx->stream));
     CK(launchBasic(p, ctx->stream));
     CK(hipEventRecord(eve, ctx->stream));
-    ctx->launches++;
+    commitLaunch(ctx);
     return PT_OK;
   }
   if (!ctx->d_bvh || !eye || !cameraRotate) return fail(ctx, ctx->d_bvh ? PT_E_INVALID : PT_E_NOSCENE, "no scene");
@@ -1019,7 +1082,7 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
                      ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, ctx->stream));
     ctx->orderValid = true;
   }
-  ctx->launches++;
+  commitLaunch(ctx);
   return PT_OK;
 }
 
@@ -1173,14 +1236,10 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   st->tri_fetch = h[2];
   st->mat_fetch = h[3];
   st->tex_fetch = h[4];
-  st->kernel_ms = 0.0f;
-  st->kernel_ms_total = 0.0f;
-  for (int k = 0; k < ctx->launches; k++) {
-    float ms = 0.0f;
-    CK(hipEventElapsedTime(&ms, ctx->evs[2 * k], ctx->evs[2 * k + 1]));
-    st->kernel_ms_total += ms;
-    st->kernel_ms = ms;
+  while (foldOne(ctx, true)) {
   }
+  st->kernel_ms = ctx->launches > 0 ? ctx->msLast : 0.0f;
+  st->kernel_ms_total = (float)ctx->msTotal;
   st->launches = ctx->launches;
   st->max_stack = ctx->maxStack;
   st->split_items = 0;
@@ -1240,7 +1299,11 @@ int pt_reset_stats(pt_ctx* ctx) {
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
   CK(hipMemset(ctx->d_ctl + CTL_STATS, 0, CTL_BYTES - CTL_STATS));
+  while (foldOne(ctx, true)) {
+  }
   ctx->launches = 0;
+  ctx->msTotal = 0.0;
+  ctx->msLast = 0.0f;
   return PT_OK;
 }
 

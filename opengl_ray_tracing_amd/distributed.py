@@ -68,35 +68,75 @@ class FrameGather:
     """RCCL gather of every rank's shard of a Renderer's accumulation to rank 0.
 
     Device buffers are torch tensors (torch is the allocator/collective
-    plumbing here); the pack/unpack kernels and the renderer run on torch's
-    current stream so the collective orders after them.
+    plumbing here). The renderer runs on torch's current stream; each call
+    packs the frame just rendered there into one of two send buffers and runs
+    the gather -- and on rank 0 the unpack into its accumulation -- on a
+    communication stream, so frame f's gather overlaps frame f+1's render
+    (rank 0's render writes only its own tiles, the unpack only the others').
+    A send buffer is packed again only after its previous gather finished.
+    `synchronize()` (or the device-wide synchronise a caller does anyway)
+    completes the last frame's gather; rank 0's accumulation then holds the
+    whole frame, bit-identical to a single-GPU render. `overlap=False` runs
+    everything on the render stream.
     """
 
-    def __init__(self, renderer, rank: int, world: int, device):
+    def __init__(self, renderer, rank: int, world: int, device, overlap: bool = True):
         import torch
         import torch.distributed as dist
 
-        self.r, self.rank, self.world, self.dist = renderer, rank, world, dist
+        self.torch, self.dist = torch, dist
+        self.r, self.rank, self.world = renderer, rank, world
         counts = [renderer.owned_pixel_count(k, world) for k in range(world)]
         self.maxc = max(counts)
-        self.send = torch.zeros((self.maxc, 4), dtype=torch.float32, device=device)
+        self.overlap = overlap and not _staged()
+        # the renderer gets a stream of its own that torch knows about (torch's default
+        # stream has the handle 0, which pt_set_stream reads as "the context's own stream")
+        self.render_stream = torch.cuda.Stream(device)
+        self.comm_stream = torch.cuda.Stream(device) if self.overlap else self.render_stream
+        nbuf = 2 if self.overlap else 1
+        self.send = [torch.zeros((self.maxc, 4), dtype=torch.float32, device=device) for _ in range(nbuf)]
+        self.sent = [None] * nbuf  # event: the buffer's last gather has completed
         self.recv = [torch.zeros((self.maxc, 4), dtype=torch.float32, device=device) for _ in range(world)] \
             if rank == 0 else None
-        renderer.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        self.k = 0
+        renderer.set_stream(self.render_stream.cuda_stream)
 
     def __call__(self):
-        self.r.pack_owned(self.send.data_ptr())
-        if _staged():  # gloo rehearsal: the collective on host copies
-            recv = [t.cpu() for t in self.recv] if self.rank == 0 else None
-            self.dist.gather(self.send.cpu(), gather_list=recv, dst=0)
+        torch, dist = self.torch, self.dist
+        i = self.k % len(self.send)
+        self.k += 1
+        buf = self.send[i]
+        if self.sent[i] is not None:
+            self.render_stream.wait_event(self.sent[i])
+        self.r.pack_owned(buf.data_ptr())  # on the render stream, after the frame
+        if _staged():  # gloo rehearsal: the collective on host copies, ordered after the pack
+            with torch.cuda.stream(self.render_stream):
+                host = buf.cpu()
+                recv = [torch.zeros_like(host) for _ in range(self.world)] if self.rank == 0 else None
+                dist.gather(host, gather_list=recv, dst=0)
+                if self.rank == 0:
+                    for t, h in zip(self.recv, recv):
+                        t.copy_(h)
+                    for k in range(1, self.world):
+                        self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
+            return
+        packed = torch.cuda.Event()
+        packed.record(self.render_stream)
+        with torch.cuda.stream(self.comm_stream):
+            self.comm_stream.wait_event(packed)
+            dist.gather(buf, gather_list=self.recv, dst=0)
             if self.rank == 0:
-                for t, h in zip(self.recv, recv):
-                    t.copy_(h)
-        else:
-            self.dist.gather(self.send, gather_list=self.recv, dst=0)
-        if self.rank == 0:
-            for k in range(1, self.world):
-                self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
+                self.r.set_stream(self.comm_stream.cuda_stream)
+                for k in range(1, self.world):
+                    self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
+                self.r.set_stream(self.render_stream.cuda_stream)
+            done = torch.cuda.Event()
+            done.record(self.comm_stream)
+        self.sent[i] = done
+
+    def synchronize(self):
+        self.comm_stream.synchronize()
+        self.render_stream.synchronize()
 
 
 def _staged() -> bool:
@@ -134,12 +174,15 @@ class SampleReduce:
         import torch
 
         self.r, self.rank, self.world = renderer, rank, world
+        self.torch = torch
         self.img = torch.empty((renderer.height, renderer.width, 4), dtype=torch.float32, device=device)
-        renderer.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        self.stream = torch.cuda.Stream(device)
+        renderer.set_stream(self.stream.cuda_stream)
 
     def __call__(self):
-        self.r.accum_into(self.img.data_ptr())
-        return combine_sample_means(self.img, self.rank, self.world)
+        self.r.accum_into(self.img.data_ptr())  # synchronous on the renderer's stream
+        with self.torch.cuda.stream(self.stream):
+            return combine_sample_means(self.img, self.rank, self.world)
 
 
 def broadcast_scene(build, rank: int, device=None):

@@ -244,3 +244,33 @@ def test_hdr_cache_on_gpu_equals_host(name):
     with Renderer(8, 8) as r:
         dev = r.hdr_cache_device(hdr)
     assert np.array_equal(dev.view(np.uint32), host.view(np.uint32))
+
+
+def test_launch_timing_ring_keeps_stats_exact():
+    """Launch times live in a fixed ring of event pairs: rendering more frames than
+    the ring holds keeps launches, the last frame's time and the summed time exact, and
+    pt_reset_stats starts the totals over."""
+    cfg, tris, nodes, hdr = scenes.build_config("c2")
+    eye, rot = orbit_camera(*cfg.camera)
+    frames = 150  # > the 64-entry ring
+    with Renderer(64, 36, "lambert") as r:
+        r.upload_scene(tris, nodes)
+        r.upload_env(hdr)
+        per = []
+        for f in range(frames):
+            r.render_frame(eye, rot, f)
+            st = r.stats()
+            assert st.launches == f + 1
+            per.append(st.kernel_ms)
+        st = r.stats()
+        assert st.launches == frames
+        assert all(ms > 0 for ms in per)
+        assert abs(st.kernel_ms_total - sum(per)) <= 1e-3 * sum(per)
+        r.reset_stats()
+        st = r.stats()
+        assert st.launches == 0 and st.kernel_ms_total == 0.0 and st.rays == 0
+        for f in range(frames):  # asynchronous frames: the ring back-pressures, nothing is lost
+            r.render_frame(eye, rot, frames + f, sync=False)
+        st = r.stats()
+        assert st.launches == frames and st.kernel_ms_total > 0
+        assert st.rays >= frames * 64 * 36
