@@ -21,8 +21,12 @@ N > 1 ranks (one process per GPU):
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver launch for N > 1)
 
 Rank 0 prints one JSON line (contract in the task statement), with
-``roofline`` (algorithmic bytes of the reference algorithm per launch / the
-kernel's HIP-event duration, against the 8 TB/s HBM peak) and ``cpu_baseline``
+``roofline`` for the frame kernel: the per-launch work the hardware counters
+measured for it (VALU wave-instructions, DRAM-side bytes; committed under
+profiles/r2/counters.json by tools/roofline.py) over its live HIP-event
+duration, against each resource's peak -- ``bound`` is the resource with the
+highest fraction -- plus ``equivalent_GBs``, the reference algorithm's fetch
+bytes per launch over the same duration; and ``cpu_baseline``
 (the CPU restatement of the reference on the host cores, rank 0 at N = 1).
 """
 from __future__ import annotations
@@ -40,6 +44,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# VALU issue: 1024 SIMD-32s (256 CUs x 4) each issue one wave64 VALU instruction per 2 cycles
+# at the 2.4 GHz maximum clock (MI355X_MICROARCH.md "Wave scheduling"): 1228.8 G wave-instructions/s
+VALU_PEAK_GINST = 1024 * 2.4 / 2 * 1e9 / 1e9
 METRIC = "Mrays/sec + ms/frame (1 spp, 1080p) at 1/2/4/8 MI355X; CPU-ref spp-matched PSNR"
 PROBE_FRAMES = 14  # frames after a restart during which the renderer measures its tree and split policies
 
@@ -55,8 +62,9 @@ def parse():
     ap.add_argument("--no-psnr", action="store_true", help="skip the spp-matched PSNR check")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="cpu_baseline sample: full frames are rendered until this much CPU wall time has passed")
-    ap.add_argument("--traffic", default=str(ROOT / "profiles" / "r1" / "traffic.json"),
-                    help="JSON with per-launch PMC HBM bytes of the bench kernel (tools/traffic.py)")
+    ap.add_argument("--counters", default=str(ROOT / "profiles" / "r2" / "counters.json"),
+                    help="per-launch PMC counters of the bench kernel per config (tools/roofline.py)")
+    ap.add_argument("--no-reset", action="store_true", help="skip the reset_ms_per_frame frames (profiling runs)")
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="rehearsal: every rank on device 0")
@@ -152,11 +160,13 @@ def main():
     # interactive cost after a camera reset (the reference zeroes frameCounter on every mouse
     # move, OpenglRayTracing/main.cpp:611-634): frames 0..PROBE_FRAMES-1 of a restarted running
     # mean, including the renderer's policy probe, timed like the steps
-    t2 = time.perf_counter()
-    for f in range(PROBE_FRAMES):
-        step(f)
-    sync_all()
-    reset_ms = 1e3 * (time.perf_counter() - t2) / PROBE_FRAMES
+    reset_ms = None
+    if not args.no_reset:
+        t2 = time.perf_counter()
+        for f in range(PROBE_FRAMES):
+            step(f)
+        sync_all()
+        reset_ms = 1e3 * (time.perf_counter() - t2) / PROBE_FRAMES
     combined_finite = None
     if combine is not None:  # the ranks' running means -> one image on rank 0 (after the timed steps)
         img = combine()
@@ -173,9 +183,10 @@ def main():
         sm = tt.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0].item())
-        rs = torch.tensor([reset_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(rs, op=dist.ReduceOp.MAX)
-        reset_ms = float(rs[0].item())
+        if reset_ms is not None:
+            rs = torch.tensor([reset_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(rs, op=dist.ReduceOp.MAX)
+            reset_ms = float(rs[0].item())
         rays_total = float(sm[1].item())
         kernel_ms_avg = float(mx[2].item()) / max(st.launches, 1)
     else:
@@ -186,15 +197,7 @@ def main():
         ms_per_step = 1e3 * elapsed / args.steps
         mrays = rays_total / elapsed / 1e6
         rays_per_launch = rays_local / max(st.launches, 1)
-        achieved = rays_per_launch * bytes_per_ray / (kernel_ms_avg * 1e-3) / 1e9
-        traffic = None
-        if args.traffic and Path(args.traffic).exists() and not args.flags and not args.builder:
-            ent = json.loads(Path(args.traffic).read_text()).get(args.config)
-            traffic = ent.get("bytes_per_launch") if ent else None
-        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "renderKernel<%s>" % cfg.integrator, "kernel_ms": round(kernel_ms_avg, 4),
-                    "bytes_per_ray": round(bytes_per_ray, 1), "rays_per_launch": int(rays_per_launch)}
+        roofline = make_roofline(args, cfg, kernel_ms_avg, rays_per_launch, bytes_per_ray, n)
         cpu = None
         if not args.no_cpu_baseline and n == 1:
             cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_seconds)
@@ -202,7 +205,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "probe_frames": PROBE_FRAMES, "ms_per_step": round(ms_per_step, 4),
-            "reset_ms_per_frame": round(reset_ms, 4),
+            "reset_ms_per_frame": None if reset_ms is None else round(reset_ms, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.shard == "tiles" else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
@@ -226,6 +229,45 @@ def main():
     r.close()
     if n > 1:
         dist.destroy_process_group()
+
+
+def make_roofline(args, cfg, kernel_ms, rays_per_launch, bytes_per_ray, n):
+    """Roofline of the frame kernel. Each resource's per-launch work comes from the hardware
+    counters of the same workload (profiles/r2/counters.json, tools/roofline.py, one rocprofv3
+    pass per counter group over this bench's timed frames); divided by this run's live kernel
+    time it gives the achieved rate:
+      valu: SQ_INSTS_VALU wave-instructions / t  vs 1228.8 G/s (1024 SIMDs x 2.4 GHz / 2 cycles)
+      hbm:  (2*FETCH_SIZE + WRITE_SIZE) KiB / t  vs 8 TB/s (gfx950 FETCH_SIZE halving corrected)
+    `bound` is the resource with the higher fraction. `equivalent_GBs` is the reference
+    algorithm's fetch bytes (48 F_node + 72 F_tri + 72 F_mat + 12 F_tex per ray,
+    counted by the instrumented kernel) over the same time -- what pass1.fsh would have to
+    move, not what this kernel moves (its tree, culling and packets fetch far less)."""
+    t = kernel_ms * 1e-3
+    eq = rays_per_launch * bytes_per_ray / t / 1e9
+    base = {"kernel": "renderKernel<%s>" % cfg.integrator, "kernel_ms": round(kernel_ms, 4),
+            "equivalent_GBs": round(eq, 1), "bytes_per_ray": round(bytes_per_ray, 1),
+            "rays_per_launch": int(rays_per_launch)}
+    ent = None
+    p = Path(args.counters) if args.counters else None
+    if p and p.exists() and not args.flags and not args.builder and n == 1:
+        ent = json.loads(p.read_text()).get(args.config)
+    if not ent:
+        return {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                "note": "no committed counters for this workload", **base}
+    cands = {
+        "valu": (ent["valu_insts"] / t / 1e9, VALU_PEAK_GINST, "G VALU wave-instructions/s"),
+        "hbm": (ent["dram_bytes"] / t / 1e9, HBM_PEAK_GBS, "GB/s"),
+    }
+    bound = max(cands, key=lambda k: cands[k][0] / cands[k][1])
+    a, pk, unit = cands[bound]
+    return {"bound": bound, "achieved": round(a, 2), "peak": pk, "unit": unit, "frac": round(a / pk, 4),
+            "traffic": int(ent["dram_bytes"]),
+            "candidates": {k: {"achieved": round(v[0], 2), "peak": v[1], "unit": v[2], "frac": round(v[0] / v[1], 4)}
+                           for k, v in cands.items()},
+            "counters": {"source": str(p.relative_to(ROOT)) if p.is_relative_to(ROOT) else str(p),
+                         "valu_insts_per_launch": ent["valu_insts"], "dram_bytes_per_launch": ent["dram_bytes"],
+                         "l2_hit": ent.get("l2_hit"), "profiled_kernel_ms": ent.get("kernel_ms")},
+            **base}
 
 
 REF_PSNR_128SPP = 20.71  # SURVEY.md 6: the reference CPU tracer at 128 spp vs its 4000spp.png

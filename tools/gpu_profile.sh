@@ -1,20 +1,29 @@
 #!/bin/bash
-# rocprofv3 evidence for the bench kernel: kernel trace + stats, then HBM
-# traffic counters in their own passes (FETCH_SIZE and WRITE_SIZE cannot share
-# a pass on gfx950). Output under gpurun_out/prof_<tag>/.
+# rocprofv3 evidence for the bench kernel of config $2 (tag $1): kernel trace +
+# stats of the bench command, then the counter groups the roofline needs, each
+# in its own rocprofv3 pass (--pmc with kernel dispatch records only; FETCH_SIZE
+# and WRITE_SIZE cannot share a pass on gfx950). Output: gpurun_out/prof_<tag>_<cfg>/.
+# Summarise with tools/roofline.py.
 set -o pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-TAG="${1:-r1}"
+TAG="${1:-r2}"
 CFG="${2:-c2}"
 OUT="$REPO/gpurun_out/prof_${TAG}_${CFG}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=(python3 "$REPO/bench.py" --config "$CFG" --steps 30 --warmup 5 --no-cpu-baseline)
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- "${BENCH[@]}" > "$OUT/trace.log" 2>&1; rc=$?
+# the bench's own flow: 14 probe frames, W warmup, K timed frames (tools/roofline.py selects those)
+BENCH=(python3 "$REPO/bench.py" --config "$CFG" --steps 30 --warmup 5 --no-cpu-baseline --no-psnr --no-reset)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- "${BENCH[@]}" > "$OUT/bench_line.json" 2> "$OUT/trace.log"; rc=$?
 echo "trace=$rc"; [ $rc -eq 0 ] || exit $rc
-BENCH5=(python3 "$REPO/bench.py" --config "$CFG" --steps 5 --warmup 2 --no-cpu-baseline)
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -f csv -d "$OUT/fetch" -o run -- "${BENCH5[@]}" > "$OUT/fetch.log" 2>&1; rc=$?
-echo "fetch=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -f csv -d "$OUT/write" -o run -- "${BENCH5[@]}" > "$OUT/write.log" 2>&1; rc=$?
-echo "write=$rc"
-exit $rc
+BENCHC=(python3 "$REPO/bench.py" --config "$CFG" --steps 10 --warmup 2 --no-cpu-baseline --no-psnr --no-reset)
+PASSES=(
+  "fetch:FETCH_SIZE"
+  "write:WRITE_SIZE"
+  "sq:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
+  "mem:TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE"
+)
+for p in "${PASSES[@]}"; do
+  name="${p%%:*}"; ctr="${p#*:}"
+  timeout -s KILL 300 rocprofv3 --pmc $ctr -f csv -d "$OUT/$name" -o run -- "${BENCHC[@]}" > "$OUT/$name.log" 2>&1; rc=$?
+  echo "pass $name=$rc"; [ $rc -eq 0 ] || exit $rc
+done

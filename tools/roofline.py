@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Roofline evidence from the rocprofv3 runs of tools/gpu_profile.sh.
+
+    python tools/roofline.py <tag> <cfg> [<cfg> ...]
+
+Reads gpurun_out/prof_<tag>_<cfg>/ and writes, under profiles/<tag>/:
+  <cfg>/kernel_stats.csv       rocprofv3 --kernel-trace --stats summary of the bench command
+  <cfg>/timed_dispatches.json  the bench kernel's dispatches of bench.py's timed region
+  <cfg>/counters.csv           every counter row of the bench kernel's timed dispatches
+  bench_<cfg>.json             the profiled run's bench line
+  counters.json                {cfg: per-launch counter averages + the derived roofline work}
+bench.py reads counters.json (--counters) and divides each resource's per-launch
+work by its own live kernel time.
+
+The bench kernel is the culling frame kernel renderKernel<I, true, false[, W]>.
+bench.py renders PROBE_FRAMES policy-probe frames, then W warmup and K timed
+frames of it, so its timed dispatches are numbers [PROBE+W, PROBE+W+K) in
+dispatch order (the fetch-counting kernel, renderKernel<I, false, true>, and
+the PSNR check's basicKernel are other kernels).
+
+Derived per-launch work (MI355X_MICROARCH.md):
+  valu_insts = SQ_INSTS_VALU (wave64 instructions; peak issue 1024 SIMDs x 2.4 GHz / 2 cycles)
+  dram_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   (KiB units; gfx950 FETCH_SIZE halving)
+  l2_hit     = TCC_HIT / (TCC_HIT + TCC_MISS);  clock_ghz = GRBM_GUI_ACTIVE / 8 / kernel time
+"""
+import csv
+import glob
+import json
+import re
+import shutil
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+OUT = ROOT / "gpurun_out"
+PROBE = 14
+TRACE_RUN = (5, 30)    # tools/gpu_profile.sh: --warmup 5 --steps 30 under --kernel-trace
+COUNTER_RUN = (2, 10)  # --warmup 2 --steps 10 under each --pmc pass
+BENCH_KERNEL = re.compile(r"renderKernel<\d+, true, false(, \d+)?>")
+
+
+def one(pattern: str) -> Path:
+    hits = sorted(glob.glob(pattern, recursive=True))
+    if not hits:
+        raise SystemExit(f"missing {pattern}")
+    return Path(hits[0])
+
+
+def timed(rows, run):
+    w, k = run
+    rows = sorted(rows, key=lambda r: int(r["Dispatch_Id"]))
+    return rows[PROBE + w:PROBE + w + k], len(rows)
+
+
+def main():
+    tag, cfgs = sys.argv[1], sys.argv[2:] or ["c2", "c4", "c5"]
+    dst = ROOT / "profiles" / tag
+    dst.mkdir(parents=True, exist_ok=True)
+    cpath = dst / "counters.json"
+    summary = json.loads(cpath.read_text()) if cpath.exists() else {}
+    for c in cfgs:
+        prof = OUT / f"prof_{tag}_{c}"
+        d = dst / c
+        d.mkdir(exist_ok=True)
+        shutil.copy(one(f"{prof}/trace/**/run_kernel_stats.csv"), d / "kernel_stats.csv")
+        trace = [r for r in csv.DictReader(open(one(f"{prof}/trace/**/run_kernel_trace.csv")))
+                 if BENCH_KERNEL.search(r["Kernel_Name"])]
+        sel, total = timed(trace, TRACE_RUN)
+        ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in sel]
+        kernel_ms = sum(ms) / len(ms)
+        (d / "timed_dispatches.json").write_text(json.dumps({
+            "kernel": sel[-1]["Kernel_Name"], "dispatches": total, "timed_dispatches": len(sel),
+            "selection": f"dispatches [{PROBE}+{TRACE_RUN[0]}, +{TRACE_RUN[1]}) of the bench kernel",
+            "timed_avg_ms": round(kernel_ms, 4), "timed_ms": [round(x, 4) for x in ms],
+            "vgpr": sel[-1].get("VGPR_Count"), "scratch": sel[-1].get("Scratch_Size")}, indent=1) + "\n")
+        line = (prof / "bench_line.json").read_text().strip().splitlines()
+        line = [ln for ln in line if ln.startswith("{")]
+        if line:
+            (dst / f"bench_{c}.json").write_text(line[-1] + "\n")
+
+        vals = defaultdict(list)
+        rows_out = []
+        header = None
+        for name in ("fetch", "write", "sq", "mem"):
+            f = one(f"{prof}/{name}/**/run_counter_collection.csv")
+            rows = list(csv.DictReader(open(f)))
+            header = header or list(rows[0].keys())
+            bench = [r for r in rows if BENCH_KERNEL.search(r["Kernel_Name"])]
+            by_disp = defaultdict(list)
+            for r in bench:
+                by_disp[r["Dispatch_Id"]].append(r)
+            disp = sorted(by_disp, key=int)
+            w, k = COUNTER_RUN
+            keep = disp[PROBE + w:PROBE + w + k]
+            for di in keep:
+                for r in by_disp[di]:
+                    vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                    rows_out.append({"pass": name, **r})
+        with open(d / "counters.csv", "w", newline="") as fh:
+            wr = csv.DictWriter(fh, fieldnames=["pass"] + header)
+            wr.writeheader()
+            wr.writerows(rows_out)
+        m = {k: sum(v) / len(v) for k, v in vals.items()}
+        g = lambda k: m.get(k, float("nan"))  # noqa: E731
+        ent = {
+            "kernel": sel[-1]["Kernel_Name"], "kernel_ms": round(kernel_ms, 4),
+            "valu_insts": round(g("SQ_INSTS_VALU")),
+            "dram_bytes": round((2 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024),
+            "l2_hit": round(g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")), 4),
+            "valu_lane_util": round(g("SQ_THREAD_CYCLES_VALU") / (64 * g("SQ_ACTIVE_INST_VALU")), 4),
+            "clock_ghz_profiled": round(g("GRBM_GUI_ACTIVE") / 8 / (kernel_ms * 1e-3) / 1e9, 3),
+            "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())},
+            "samples": {k: len(v) for k, v in sorted(vals.items())},
+            "derivation": "valu_insts = SQ_INSTS_VALU; dram_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024; "
+                          "per launch, averaged over the bench kernel's timed dispatches of each pass",
+        }
+        summary[c] = ent
+        print(c, json.dumps({k: ent[k] for k in ("kernel_ms", "valu_insts", "dram_bytes", "l2_hit",
+                                                  "valu_lane_util", "clock_ghz_profiled")}))
+    cpath.write_text(json.dumps(summary, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
