@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats */
 
 /* error codes */
 #define PT_OK 0
@@ -53,6 +53,12 @@ extern "C" {
 #define PT_FLAG_NO_TILE_ORDER 0x20u /* megakernel: hand out tiles in fixed order, not longest-first */
 #define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */
 
+/* in-process multi-GPU (pt_config.n_devices > 1) */
+#define PT_MAX_DEVICES 8
+#define PT_GATHER_AUTO 0  /* RCCL send/recv when the devices are distinct and RCCL loads, else peer copies */
+#define PT_GATHER_COPY 1  /* hipMemcpyPeerAsync of each device's packed tiles to the first device (xGMI) */
+#define PT_GATHER_RCCL 2  /* RCCL send/recv group (ncclCommInitAll over device_ids); error if unavailable */
+
 typedef struct pt_config {
   int width;          /* RenderPass::width  (OpenglRayTracing/main.cpp:83), e.g. 1920 */
   int height;         /* RenderPass::height (OpenglRayTracing/main.cpp:84), e.g. 1080 */
@@ -68,6 +74,15 @@ typedef struct pt_config {
   int sample_rank;    /* sample-parallel rendering: this context draws the RNG/Sobol streams of   */
   int sample_world;   /* samples frameCounter*sample_world + sample_rank (0/1 = the reference's   */
                       /* frameCounter itself); the running-mean weight stays 1/(frameCounter+1)   */
+  /* In-process multi-GPU: n_devices >= 2 makes this one context drive
+   * device_ids[0..n_devices-1] (device_id is ignored; ids may repeat). Device k renders the
+   * 32x32 screen tiles t with t % n_devices == k; every pt_render_frame then gathers the
+   * other devices' tiles into device_ids[0]'s accumulation (gather = PT_GATHER_*), so the
+   * context's image is bit-identical to a one-device render. tile_world and sample_world
+   * must be <= 1 with n_devices >= 2. 0 or 1 = one device (device_id). */
+  int n_devices;
+  int device_ids[PT_MAX_DEVICES];
+  int gather;
 } pt_config;
 
 /* Counters accumulate over every launch since pt_create / pt_reset_stats. */
@@ -87,6 +102,8 @@ typedef struct pt_frame_stats {
                            (results checked against the uploaded one), 0 the uploaded tree */
   int waves_per_simd;   /* megakernel: waves per SIMD the last frame's kernel was compiled for
                            (3 = the large-scene Disney/MIS variant, else its default bound) */
+  int devices;          /* devices the context renders on (1, or pt_config.n_devices) */
+  int gather;           /* PT_GATHER_COPY / PT_GATHER_RCCL in use (0 with one device) */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;
@@ -97,6 +114,7 @@ int pt_create(pt_ctx** out, const pt_config* cfg);
 void pt_destroy(pt_ctx* ctx);
 const char* pt_last_error(pt_ctx* ctx);  /* ctx may be NULL: last create error */
 int pt_device_count(int* n);
+int pt_abi_version(void);  /* PT_ABI_VERSION of the loaded library */
 
 /* Upload the encoded scene (replaces the two GL_RGB32F texture buffers,
  * OpenglRayTracing/main.cpp:720-735). tris = nTriangles x 36 f32 exactly as
@@ -146,10 +164,12 @@ int pt_accum_device_ptr(pt_ctx* ctx, void** dptr); /* width*height*4 f32, device
  * = width x height x 3 f32 host buffer. */
 int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out);
 
-/* Multi-GPU tile exchange: pack this rank's owned pixels into a contiguous
- * device buffer (count = pt_owned_pixel_count), and unpack another rank's
- * packed pixels into this context's accumulation. Pointers are device memory;
- * the caller moves the packed buffers (RCCL gather over xGMI). */
+/* Multi-process tile exchange (one process per GPU, pt_config.tile_rank/tile_world):
+ * pack this rank's owned pixels into a contiguous device buffer (count =
+ * pt_owned_pixel_count), and unpack another rank's packed pixels into this
+ * context's accumulation. Pointers are device memory; the caller moves the
+ * packed buffers (RCCL gather over xGMI). Not for n_devices > 1 contexts, which
+ * gather inside pt_render_frame. */
 int pt_owned_pixel_count(pt_ctx* ctx, int rank, int world, int64_t* count);
 int pt_pack_owned(pt_ctx* ctx, void* dpacked);
 int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked);

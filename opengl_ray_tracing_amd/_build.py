@@ -49,7 +49,8 @@ SOURCES = {
                                                    INCLUDE / "pt_fmath.h"]),
     "pt_envcache.o": ("hip", CSRC / "pt_envcache.hip", [CSRC / "pt_kernels.h"]),
     "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", CSRC / "pt_wavefront.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
-                                                       INCLUDE / "pt_fmath.h"]),
+                                                       INCLUDE / "pt_fmath.h", CSRC / "pt_rccl.h"]),
+    "pt_rccl.o": ("cxx", CSRC / "pt_rccl.cpp", [CSRC / "pt_rccl.h"]),
     "scene.o": ("cxx", CSRC / "scene.cpp", [INCLUDE / "pt_scene.h"]),
 }
 
@@ -88,7 +89,7 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
                 if verbose and (r.stdout or r.stderr):
                     sys.stderr.write(r.stdout + r.stderr)
     if force or jobs or _stale(LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(LIB), *map(str, objs)])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(LIB), *map(str, objs), "-ldl"])
     return LIB
 
 
@@ -116,7 +117,7 @@ def build_variant(name: str, defines: dict, hip_flags=()) -> Path:
         else:
             _run(["g++", *CXX_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
     lib = variant_lib(name)
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(lib), *map(str, objs)])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(lib), *map(str, objs), "-ldl"])
     return lib
 
 

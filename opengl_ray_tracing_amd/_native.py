@@ -13,6 +13,7 @@ from . import _build
 
 _lib = None
 
+ABI_VERSION = 2  # include/pt_abi.h PT_ABI_VERSION
 c_float_p = C.POINTER(C.c_float)
 c_int_p = C.POINTER(C.c_int)
 
@@ -23,6 +24,7 @@ class PtConfig(C.Structure):
         ("device_id", C.c_int), ("tile_rank", C.c_int), ("tile_world", C.c_int), ("tile_size", C.c_int),
         ("flags", C.c_uint32), ("basic_samples", C.c_int), ("basic_seed", C.c_uint32),
         ("sample_rank", C.c_int), ("sample_world", C.c_int),
+        ("n_devices", C.c_int), ("device_ids", C.c_int * 8), ("gather", C.c_int),
     ]
 
 
@@ -32,7 +34,7 @@ class PtFrameStats(C.Structure):
         ("mat_fetch", C.c_uint64), ("tex_fetch", C.c_uint64), ("kernel_ms", C.c_float),
         ("kernel_ms_total", C.c_float), ("launches", C.c_int), ("max_stack", C.c_int),
         ("split_items", C.c_int), ("runtime_tree", C.c_int),
-        ("waves_per_simd", C.c_int),
+        ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int),
     ]
 
 
@@ -50,6 +52,7 @@ class PtMaterial(C.Structure):
 SIGNATURES = {
     # pt_abi.h
     "pt_device_count": (C.c_int, [c_int_p]),
+    "pt_abi_version": (C.c_int, []),
     "pt_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(PtConfig)]),
     "pt_destroy": (None, [C.c_void_p]),
     "pt_last_error": (C.c_char_p, [C.c_void_p]),
@@ -147,6 +150,8 @@ def load(build_if_missing: bool = False):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.pt_abi_version() != ABI_VERSION:  # the structs below must match the library's
+        raise RuntimeError(f"{path} has ABI {lib.pt_abi_version()}, this binding {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

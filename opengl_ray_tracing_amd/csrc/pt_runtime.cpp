@@ -19,6 +19,7 @@
 #include "pt_accel.h"
 #include "pt_fmath.h"
 #include "pt_kernels.h"
+#include "pt_rccl.h"
 #include "pt_scene.h"
 #include "pt_wavefront.h"
 
@@ -108,6 +109,40 @@ struct pt_ctx {
   WFState wf{};
   WFQueues wfq{};
   bool wfReady = false;
+  // in-process multi-GPU (pt_config.n_devices > 1): this context renders as
+  // screen-tile rank 0 on device_ids[0] and owns the other ranks' contexts and
+  // the per-frame gather of their tiles into its accumulation
+  std::vector<pt_ctx*> peers;  // ranks 1 .. n_devices-1
+  struct GroupGather* gather = nullptr;
+};
+
+// The per-frame gather of an in-process device group. Rank k >= 1 packs its
+// tiles (packKernel) on its render stream into one of two send buffers; the
+// packed tiles travel to rank 0's device -- an RCCL send/recv group over the
+// communicator of all the devices, or hipMemcpyPeerAsync -- and are unpacked
+// into rank 0's accumulation on rank 0's communication stream. Rank 0's next
+// frame renders meanwhile (its own tiles only); a send buffer is packed again
+// only after its previous transfer completed.
+struct GroupGather {
+  int mode = PT_GATHER_COPY;
+  int n = 0;
+  hipStream_t cstream = nullptr;  // rank 0's device: receives, copies, unpacks
+  hipEvent_t done = nullptr;      // rank 0's device: the last frame's unpacks
+  bool pending = false;
+  unsigned frame = 0;
+  struct Peer {
+    int dev = 0;
+    size_t count = 0;                       // packed pixels (float4) of this rank
+    float4* send[2] = {nullptr, nullptr};   // on the rank's device
+    float4* recv = nullptr;                 // on rank 0's device
+    hipStream_t mstream = nullptr;          // the rank's device: RCCL sends
+    hipEvent_t packed[2] = {nullptr, nullptr};
+    hipEvent_t sent[2] = {nullptr, nullptr};  // the buffer's transfer completed
+    bool sentValid[2] = {false, false};
+  };
+  std::vector<Peer> peer;  // ranks 1 .. n-1
+  ncclComm_t comms[PT_MAX_DEVICES] = {};
+  bool commsReady = false;
 };
 
 static std::string g_create_err;
@@ -156,7 +191,7 @@ int pt_device_count(int* n) {
 
 const char* pt_last_error(pt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
-int pt_create(pt_ctx** out, const pt_config* cfg) {
+static int createOne(pt_ctx** out, const pt_config* cfg) {
   if (!out || !cfg) return PT_E_INVALID;
   *out = nullptr;
   // width, height < 65536: the megakernel packs a pixel as (px | py << 16)
@@ -222,8 +257,56 @@ int pt_create(pt_ctx** out, const pt_config* cfg) {
   return PT_OK;
 }
 
+static void destroyGroup(pt_ctx* ctx);
+static int createGroup(pt_ctx* ctx);
+
+int pt_create(pt_ctx** out, const pt_config* cfg) {
+  if (!out || !cfg) return PT_E_INVALID;
+  *out = nullptr;
+  const int n = cfg->n_devices;
+  if (n < 0 || n > PT_MAX_DEVICES || cfg->gather < PT_GATHER_AUTO || cfg->gather > PT_GATHER_RCCL) {
+    g_create_err = "pt_create: n_devices must be 0..8 and gather a PT_GATHER_* value";
+    return PT_E_INVALID;
+  }
+  if (n <= 1) return createOne(out, cfg);
+  if (cfg->tile_world > 1 || cfg->sample_world > 1 || cfg->integrator == PT_BASIC_CPU_COMPAT) {
+    g_create_err = "pt_create: n_devices > 1 renders screen tiles of the GL integrators itself "
+                   "(tile_world and sample_world must be <= 1)";
+    return PT_E_INVALID;
+  }
+  // rank k: device_ids[k], screen tiles t % n == k
+  pt_config c = *cfg;
+  c.n_devices = 0;
+  c.tile_world = n;
+  c.tile_rank = 0;
+  c.device_id = cfg->device_ids[0];
+  int rc = createOne(out, &c);
+  if (rc) return rc;
+  pt_ctx* ctx = *out;
+  ctx->cfg.n_devices = n;
+  for (int k = 1; k < n; k++) {
+    c.tile_rank = k;
+    c.device_id = cfg->device_ids[k];
+    pt_ctx* p = nullptr;
+    if ((rc = createOne(&p, &c)) != PT_OK) {
+      pt_destroy(ctx);
+      *out = nullptr;
+      return rc;
+    }
+    ctx->peers.push_back(p);
+  }
+  if ((rc = createGroup(ctx)) != PT_OK) {
+    g_create_err = ctx->err;
+    pt_destroy(ctx);
+    *out = nullptr;
+    return rc;
+  }
+  return PT_OK;
+}
+
 void pt_destroy(pt_ctx* ctx) {
   if (!ctx) return;
+  destroyGroup(ctx);
   (void)hipSetDevice(ctx->cfg.device_id);
   if (ctx->own) (void)hipStreamSynchronize(ctx->own);
   dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
@@ -446,17 +529,32 @@ static void buildPairs(const std::vector<float4>& geo, const int* order, int nTr
   }
 }
 
+// Everything pt_upload_scene derives on the host from the caller's arrays,
+// computed once and uploaded to every device of a context.
+struct SceneHost {
+  int nTri = 0, nNodes = 0;
+  std::vector<float4> geo, pairs;
+  WideTree ref;
+  // the runtime's own tree and the reference facts its results are checked against
+  bool fast = false;
+  WideTree fastTree;
+  std::vector<float4> fpairs, refBox, leafBox;
+  std::vector<int> order, leafOf, parent;
+};
+
 // The runtime's own tree (a binned-SAH build over the uploaded triangles) and
 // the reference facts a result found through it is checked against
 // (pt_trace.h refReachable): each triangle's reference leaf and its box, every
 // reference node's parent and box. Any triangle in two reference leaves, or a
-// failed build, leaves the runtime on the reference tree alone.
-static int uploadAccel(pt_ctx* ctx, const float* tris, int nTri, const float* nodes, int nNodes,
-                       const std::vector<float4>& geo) {
-  ctx->fastReady = false;
-  if (!PT_FAST_TREE) return PT_OK;
+// failed build, leaves the runtime on the reference tree alone (h.fast false).
+static void prepareAccel(const float* tris, int nTri, const float* nodes, int nNodes, SceneHost& h) {
+  h.fast = false;
+  if (!PT_FAST_TREE) return;
   auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
-  std::vector<int> leafOf(nTri, -1), parent(nNodes, 0);
+  std::vector<int>& leafOf = h.leafOf;
+  std::vector<int>& parent = h.parent;
+  leafOf.assign(nTri, -1);
+  parent.assign(nNodes, 0);
   {
     std::vector<int> st{1};
     while (!st.empty()) {
@@ -465,7 +563,7 @@ static int uploadAccel(pt_ctx* ctx, const float* tris, int nTri, const float* no
       if (nodeN(k) > 0) {
         const int index = (int)nodes[(size_t)k * 12 + 4];
         for (int i = index; i < index + nodeN(k); i++) {
-          if (leafOf[i] != -1) return PT_OK;  // a triangle in two leaves: reference tree only
+          if (leafOf[i] != -1) return;  // a triangle in two leaves: reference tree only
           leafOf[i] = k;
         }
         continue;
@@ -478,32 +576,32 @@ static int uploadAccel(pt_ctx* ctx, const float* tris, int nTri, const float* no
           const float* pb = nodes + (size_t)k * 12;
           const float* cb = nodes + (size_t)ch * 12;
           for (int a = 0; a < 3; a++)
-            if (!(pb[6 + a] <= cb[6 + a] && cb[9 + a] <= pb[9 + a])) return PT_OK;
+            if (!(pb[6 + a] <= cb[6 + a] && cb[9 + a] <= pb[9 + a])) return;
           parent[ch] = k;
           st.push_back(ch);
         }
       }
     }
   }
-  std::vector<float4> refBox((size_t)nNodes * 2), leafBox((size_t)nTri * 2);
+  h.refBox.assign((size_t)nNodes * 2, make_float4(0, 0, 0, 0));
+  h.leafBox.assign((size_t)nTri * 2, make_float4(0, 0, 0, 0));
   for (int k = 0; k < nNodes; k++) {
     const float* c = nodes + (size_t)k * 12;
-    refBox[2 * (size_t)k] = make_float4(c[6], c[7], c[8], 0.0f);
-    refBox[2 * (size_t)k + 1] = make_float4(c[9], c[10], c[11], 0.0f);
+    h.refBox[2 * (size_t)k] = make_float4(c[6], c[7], c[8], 0.0f);
+    h.refBox[2 * (size_t)k + 1] = make_float4(c[9], c[10], c[11], 0.0f);
   }
   const float inf = INFINITY;
   for (int i = 0; i < nTri; i++) {
     if (leafOf[i] < 0) {  // in no reference leaf: never a reference hit (empty box fails the margin test)
-      leafBox[2 * (size_t)i] = make_float4(inf, inf, inf, 0.0f);
-      leafBox[2 * (size_t)i + 1] = make_float4(-inf, -inf, -inf, 0.0f);
+      h.leafBox[2 * (size_t)i] = make_float4(inf, inf, inf, 0.0f);
+      h.leafBox[2 * (size_t)i + 1] = make_float4(-inf, -inf, -inf, 0.0f);
     } else {
-      leafBox[2 * (size_t)i] = refBox[2 * (size_t)leafOf[i]];
-      leafBox[2 * (size_t)i + 1] = refBox[2 * (size_t)leafOf[i] + 1];
+      h.leafBox[2 * (size_t)i] = h.refBox[2 * (size_t)leafOf[i]];
+      h.leafBox[2 * (size_t)i + 1] = h.refBox[2 * (size_t)leafOf[i] + 1];
     }
   }
   std::vector<float> an;
-  std::vector<int> order;
-  if (pt::buildAccel(tris, nTri, PT_ACCEL_LEAF, an, order) < 0 || an.size() / 12 >= (1u << 24)) return PT_OK;
+  if (pt::buildAccel(tris, nTri, PT_ACCEL_LEAF, an, h.order) < 0 || an.size() / 12 >= (1u << 24)) return;
 
   // widened by 1e-5 of each box's own magnitude plus 3e-5 of the scene's: above
   // the rounding of a slab test (~1.2e-7 x the origin-box distance) for ray origins
@@ -511,62 +609,89 @@ static int uploadAccel(pt_ctx* ctx, const float* tris, int nTri, const float* no
   float sceneScale = 0.0f;
   for (int i = 0; i < nTri; i++)
     for (int k = 0; k < 9; k++) sceneScale = std::max(sceneScale, std::fabs(tris[(size_t)i * 36 + k]));
-  WideTree fast;
   // (a tree whose planes do not quantize is not used: the traversal's record kind is FAST_QUANT)
-  if (!encodeWideTree(an.data(), (int)(an.size() / 12), nTri, 1e-5f, fast, 3e-5f * sceneScale, FAST_QUANT).empty())
-    return PT_OK;
-  std::vector<float4> fpairs;
-  buildPairs(geo, order.data(), nTri, fpairs);
+  if (!encodeWideTree(an.data(), (int)(an.size() / 12), nTri, 1e-5f, h.fastTree, 3e-5f * sceneScale, FAST_QUANT)
+           .empty())
+    return;
+  buildPairs(h.geo, h.order.data(), nTri, h.fpairs);
+  h.fast = true;
+}
+
+// host-side re-layout of the caller's arrays (pt_upload_scene); "" or the reason they are malformed
+static std::string prepareScene(const float* tris, int nTri, const float* nodes, int nNodes, SceneHost& h) {
+  h.nTri = nTri;
+  h.nNodes = nNodes;
+  // geometry records (+1 zero record past the last triangle)
+  h.geo.assign((size_t)(nTri + 1) * 4, make_float4(0, 0, 0, 0));
+  for (int i = 0; i < nTri; i++) {
+    const float* t = tris + (size_t)i * 36;
+    float N[3];
+    nrm3(t, t + 3, t + 6, N);
+    float w = (N[0] * t[0] + N[1] * t[1]) + N[2] * t[2];
+    h.geo[4 * i + 0] = make_float4(t[0], t[1], t[2], w);
+    h.geo[4 * i + 1] = make_float4(t[3], t[4], t[5], 0.0f);
+    h.geo[4 * i + 2] = make_float4(t[6], t[7], t[8], 0.0f);
+    h.geo[4 * i + 3] = make_float4(N[0], N[1], N[2], 0.0f);
+  }
+  std::string bad = encodeWideTree(nodes, nNodes, nTri, 0.0f, h.ref);
+  if (!bad.empty()) return bad;
+  buildPairs(h.geo, nullptr, nTri, h.pairs);
+  prepareAccel(tris, nTri, nodes, nNodes, h);
+  return "";
+}
+
+static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
+  CK(hipSetDevice(ctx->cfg.device_id));
   int rc;
-  if ((rc = upload(ctx, &ctx->d_fbvh, fast.bvh)) || (rc = upload(ctx, &ctx->d_fpairs, fpairs)) ||
-      (rc = upload(ctx, &ctx->d_fastTri, order)) || (rc = upload(ctx, &ctx->d_refLeafOf, leafOf)) ||
-      (rc = upload(ctx, &ctx->d_refParent, parent)) || (rc = upload(ctx, &ctx->d_refBox, refBox)) ||
-      (rc = upload(ctx, &ctx->d_leafBox, leafBox)))
+  if ((rc = upload(ctx, &ctx->d_pairs, h.pairs)) || (rc = upload(ctx, &ctx->d_geo, h.geo)) ||
+      (rc = upload(ctx, &ctx->d_bvh, h.ref.bvh)))
     return rc;
-  ctx->fRoot = fast.rootRef;
-  ctx->fnDev = fast.nDev;
-  ctx->fDepth = fast.depth;
-  ctx->maxStack = std::max(ctx->maxStack, fast.depth + 1);
+  dfree(ctx->d_attr);
+  CK(hipMalloc(&ctx->d_attr, (size_t)h.nTri * 36 * sizeof(float)));
+  CK(hipMemcpy(ctx->d_attr, tris, (size_t)h.nTri * 36 * sizeof(float), hipMemcpyHostToDevice));
+  ctx->nTri = h.nTri;
+  ctx->nNodes = h.nNodes;
+  ctx->nDevNodes = h.ref.nDev;
+  ctx->rootRef = h.ref.rootRef;
+  ctx->depth = h.ref.depth;
+  ctx->maxStack = h.ref.depth + 1;
+  ctx->fastReady = false;
+  if (!h.fast) return PT_OK;
+  if ((rc = upload(ctx, &ctx->d_fbvh, h.fastTree.bvh)) || (rc = upload(ctx, &ctx->d_fpairs, h.fpairs)) ||
+      (rc = upload(ctx, &ctx->d_fastTri, h.order)) || (rc = upload(ctx, &ctx->d_refLeafOf, h.leafOf)) ||
+      (rc = upload(ctx, &ctx->d_refParent, h.parent)) || (rc = upload(ctx, &ctx->d_refBox, h.refBox)) ||
+      (rc = upload(ctx, &ctx->d_leafBox, h.leafBox)))
+    return rc;
+  ctx->fRoot = h.fastTree.rootRef;
+  ctx->fnDev = h.fastTree.nDev;
+  ctx->fDepth = h.fastTree.depth;
+  ctx->maxStack = std::max(ctx->maxStack, h.fastTree.depth + 1);
   ctx->fastReady = true;
   return PT_OK;
+}
+
+// every context of a device group (rank 0 first), or just ctx
+static std::vector<pt_ctx*> members(pt_ctx* ctx) {
+  std::vector<pt_ctx*> m{ctx};
+  m.insert(m.end(), ctx->peers.begin(), ctx->peers.end());
+  return m;
+}
+
+static int fromPeer(pt_ctx* ctx, pt_ctx* p, int rc) {
+  if (rc && p != ctx) ctx->err = "device " + std::to_string(p->cfg.device_id) + ": " + p->err;
+  return rc;
 }
 
 int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes, int nNodes) {
   if (!ctx || !tris || !nodes) return PT_E_INVALID;
   if (nTri < 1 || nNodes < 2) return fail(ctx, PT_E_BADSCENE, "need >= 1 triangle and >= 2 nodes (dummy 0, root 1)");
   if (nTri > MAX_TRIS) return fail(ctx, PT_E_BADSCENE, "too many triangles for the leaf encoding");
-  CK(hipSetDevice(ctx->cfg.device_id));
-  // geometry records (+1 zero record past the last triangle)
-  std::vector<float4> geo((size_t)(nTri + 1) * 4, make_float4(0, 0, 0, 0));
-  for (int i = 0; i < nTri; i++) {
-    const float* t = tris + (size_t)i * 36;
-    float N[3];
-    nrm3(t, t + 3, t + 6, N);
-    float w = (N[0] * t[0] + N[1] * t[1]) + N[2] * t[2];
-    geo[4 * i + 0] = make_float4(t[0], t[1], t[2], w);
-    geo[4 * i + 1] = make_float4(t[3], t[4], t[5], 0.0f);
-    geo[4 * i + 2] = make_float4(t[6], t[7], t[8], 0.0f);
-    geo[4 * i + 3] = make_float4(N[0], N[1], N[2], 0.0f);
-  }
-  WideTree ref;
-  std::string bad = encodeWideTree(nodes, nNodes, nTri, 0.0f, ref);
+  SceneHost h;
+  std::string bad = prepareScene(tris, nTri, nodes, nNodes, h);
   if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
-  std::vector<float4> pairs;
-  buildPairs(geo, nullptr, nTri, pairs);
-  int rc;
-  if ((rc = upload(ctx, &ctx->d_pairs, pairs)) || (rc = upload(ctx, &ctx->d_geo, geo)) ||
-      (rc = upload(ctx, &ctx->d_bvh, ref.bvh)))
-    return rc;
-  dfree(ctx->d_attr);
-  CK(hipMalloc(&ctx->d_attr, (size_t)nTri * 36 * sizeof(float)));
-  CK(hipMemcpy(ctx->d_attr, tris, (size_t)nTri * 36 * sizeof(float), hipMemcpyHostToDevice));
-  ctx->nTri = nTri;
-  ctx->nNodes = nNodes;
-  ctx->nDevNodes = ref.nDev;
-  ctx->rootRef = ref.rootRef;
-  ctx->depth = ref.depth;
-  ctx->maxStack = ref.depth + 1;
-  return uploadAccel(ctx, tris, nTri, nodes, nNodes, geo);
+  for (pt_ctx* m : members(ctx))
+    if (int rc = uploadScene(m, tris, h)) return fromPeer(ctx, m, rc);
+  return PT_OK;
 }
 
 // calculateHdrCache of host image hdr (w*h*3) into the device table out (w*h float4)
@@ -588,7 +713,7 @@ static int deviceHdrCache(pt_ctx* ctx, const float* hdr, int w, int h, float4* o
   return PT_OK;
 }
 
-int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache) {
+static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache) {
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   dfree(ctx->d_hdr);
@@ -625,6 +750,21 @@ int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
   return PT_OK;
 }
 
+int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache) {
+  if (!ctx) return PT_E_INVALID;
+  if (ctx->peers.empty()) return envOne(ctx, hdr, w, h, cache);
+  // a device group computes calculateHdrCache once (on rank 0's GPU) and uploads it everywhere
+  std::vector<float> own;
+  if (hdr && !cache && w > 0 && h > 0) {
+    own.resize((size_t)w * h * 3);
+    if (int rc = pt_hdr_cache_device(ctx, hdr, w, h, own.data())) return rc;
+    cache = own.data();
+  }
+  for (pt_ctx* m : members(ctx))
+    if (int rc = envOne(m, hdr, w, h, cache)) return fromPeer(ctx, m, rc);
+  return PT_OK;
+}
+
 int pt_hdr_cache_device(pt_ctx* ctx, const float* hdr, int w, int h, float* cache_out) {
   if (!ctx || !hdr || !cache_out || w <= 0 || h <= 0) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
@@ -647,6 +787,7 @@ int pt_hdr_cache_device(pt_ctx* ctx, const float* hdr, int w, int h, float* cach
 
 int pt_upload_shapes(pt_ctx* ctx, const float* shapes, int n) {
   if (!ctx || (!shapes && n > 0) || n < 0) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "BASIC shapes: one device only");
   CK(hipSetDevice(ctx->cfg.device_id));
   dfree(ctx->d_shapes);
   ctx->nShapes = 0;
@@ -942,7 +1083,7 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
   return f >= 6 ? PT_SPLIT_PCT : 0;
 }
 
-int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
+static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   const pt_config& c = ctx->cfg;
@@ -1086,6 +1227,17 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   return PT_OK;
 }
 
+static int groupGather(pt_ctx* ctx);
+
+int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
+  if (!ctx) return PT_E_INVALID;
+  if (ctx->peers.empty()) return renderOne(ctx, eye, cameraRotate, frameCounter);
+  // every device renders its tiles on its own stream; then the gather (GroupGather)
+  for (pt_ctx* m : members(ctx))
+    if (int rc = renderOne(m, eye, cameraRotate, frameCounter)) return fromPeer(ctx, m, rc);
+  return groupGather(ctx);
+}
+
 int pt_render_frame(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter,
                     float* accum_rgba) {
   int rc = pt_render_frame_async(ctx, eye, cameraRotate, frameCounter);
@@ -1129,8 +1281,18 @@ int pt_trace_closest(pt_ctx* ctx, const float* rays, int n, float* t_out, int* t
   return PT_OK;
 }
 
+// a device group's rank-0 stream waits for the last gather (the whole image is in its accumulation)
+static int joinGather(pt_ctx* ctx) {
+  GroupGather* g = ctx->gather;
+  if (!g || !g->pending) return PT_OK;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  CK(hipStreamWaitEvent(ctx->stream, g->done, 0));
+  return PT_OK;
+}
+
 int pt_download_accum(pt_ctx* ctx, float* accum) {
   if (!ctx || !accum) return PT_E_INVALID;
+  if (int rc = joinGather(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
   CK(hipMemcpyAsync(accum, ctx->d_accum, bytes, hipMemcpyDefault, ctx->stream));  // host or device
@@ -1138,8 +1300,7 @@ int pt_download_accum(pt_ctx* ctx, float* accum) {
   return PT_OK;
 }
 
-int pt_upload_accum(pt_ctx* ctx, const float* accum) {
-  if (!ctx || !accum) return PT_E_INVALID;
+static int uploadAccumOne(pt_ctx* ctx, const float* accum) {
   CK(hipSetDevice(ctx->cfg.device_id));
   const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
   CK(hipMemcpyAsync(ctx->d_accum, accum, bytes, hipMemcpyDefault, ctx->stream));  // host or device
@@ -1147,10 +1308,23 @@ int pt_upload_accum(pt_ctx* ctx, const float* accum) {
   return PT_OK;
 }
 
+// (every device of a group takes the whole image: each continues the running mean of its own tiles)
+int pt_upload_accum(pt_ctx* ctx, const float* accum) {
+  if (!ctx || !accum) return PT_E_INVALID;
+  if (int rc = joinGather(ctx)) return rc;
+  for (pt_ctx* m : members(ctx))
+    if (int rc = uploadAccumOne(m, accum)) return fromPeer(ctx, m, rc);
+  return PT_OK;
+}
+
 int pt_clear_accum(pt_ctx* ctx) {
   if (!ctx) return PT_E_INVALID;
-  CK(hipSetDevice(ctx->cfg.device_id));
-  CK(hipMemsetAsync(ctx->d_accum, 0, (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4), ctx->stream));
+  if (int rc = joinGather(ctx)) return rc;
+  for (pt_ctx* m : members(ctx)) {
+    if (hipSetDevice(m->cfg.device_id) != hipSuccess ||
+        hipMemsetAsync(m->d_accum, 0, (size_t)m->cfg.width * m->cfg.height * sizeof(float4), m->stream) != hipSuccess)
+      return fail(ctx, PT_E_HIP, "pt_clear_accum on device " + std::to_string(m->cfg.device_id));
+  }
   return PT_OK;
 }
 
@@ -1162,6 +1336,7 @@ int pt_accum_device_ptr(pt_ctx* ctx, void** dptr) {
 
 int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out) {
   if (!ctx || !rgb_out || !(limit > 0.0f)) return PT_E_INVALID;
+  if (int rc = joinGather(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   const int n = ctx->cfg.width * ctx->cfg.height;
   if (!ctx->d_rgb) CK(hipMalloc(&ctx->d_rgb, (size_t)n * 3 * sizeof(float)));
@@ -1187,12 +1362,14 @@ static PackParams packParams(const pt_ctx* ctx, int rank, int world) {
 
 int pt_owned_pixel_count(pt_ctx* ctx, int rank, int world, int64_t* count) {
   if (!ctx || !count || world < 1 || rank < 0 || rank >= world) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
   *count = packParams(ctx, rank, world).count;
   return PT_OK;
 }
 
 int pt_pack_owned(pt_ctx* ctx, void* dpacked) {
   if (!ctx || !dpacked) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
   CK(hipSetDevice(ctx->cfg.device_id));
   PackParams p = packParams(ctx, ctx->cfg.tile_rank, ctx->cfg.tile_world);
   CK(launchPack(p, ctx->d_accum, reinterpret_cast<float4*>(dpacked), ctx->stream));
@@ -1201,6 +1378,7 @@ int pt_pack_owned(pt_ctx* ctx, void* dpacked) {
 
 int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked) {
   if (!ctx || !dpacked || world < 1 || rank < 0 || rank >= world) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
   CK(hipSetDevice(ctx->cfg.device_id));
   PackParams p = packParams(ctx, rank, world);
   CK(launchUnpack(p, ctx->d_accum, reinterpret_cast<const float4*>(dpacked), ctx->stream));
@@ -1213,15 +1391,62 @@ int pt_set_stream(pt_ctx* ctx, void* s) {
   return PT_OK;
 }
 
-int pt_synchronize(pt_ctx* ctx) {
-  if (!ctx) return PT_E_INVALID;
+static int syncOne(pt_ctx* ctx) {
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
   return PT_OK;
 }
 
+// a group: every device's render stream, the gather's streams, then rank 0's stream
+static int syncGroup(pt_ctx* ctx) {
+  for (pt_ctx* p : ctx->peers)
+    if (int rc = syncOne(p)) return fromPeer(ctx, p, rc);
+  if (GroupGather* g = ctx->gather) {
+    for (auto& P : g->peer)
+      if (P.mstream) {
+        CK(hipSetDevice(P.dev));
+        CK(hipStreamSynchronize(P.mstream));
+      }
+    CK(hipSetDevice(ctx->cfg.device_id));
+    CK(hipStreamSynchronize(g->cstream));
+    g->pending = false;
+  }
+  return syncOne(ctx);
+}
+
+int pt_synchronize(pt_ctx* ctx) {
+  if (!ctx) return PT_E_INVALID;
+  return ctx->peers.empty() ? syncOne(ctx) : syncGroup(ctx);
+}
+
+static int statsOne(pt_ctx* ctx, pt_frame_stats* st);
+
+// A group: rays and fetches summed over the devices, kernel times the slowest device's,
+// launches / policies rank 0's.
 int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   if (!ctx || !st) return PT_E_INVALID;
+  if (ctx->peers.empty()) return statsOne(ctx, st);
+  if (int rc = syncGroup(ctx)) return rc;
+  if (int rc = statsOne(ctx, st)) return rc;
+  for (pt_ctx* p : ctx->peers) {
+    pt_frame_stats q;
+    if (int rc = statsOne(p, &q)) return fromPeer(ctx, p, rc);
+    st->rays += q.rays;
+    st->node_fetch += q.node_fetch;
+    st->tri_fetch += q.tri_fetch;
+    st->mat_fetch += q.mat_fetch;
+    st->tex_fetch += q.tex_fetch;
+    st->kernel_ms = std::max(st->kernel_ms, q.kernel_ms);
+    st->kernel_ms_total = std::max(st->kernel_ms_total, q.kernel_ms_total);
+    st->max_stack = std::max(st->max_stack, q.max_stack);
+    st->split_items += q.split_items;
+  }
+  st->devices = 1 + (int)ctx->peers.size();
+  st->gather = ctx->gather ? ctx->gather->mode : 0;
+  return PT_OK;
+}
+
+static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
   unsigned long long h[5];
@@ -1245,6 +1470,8 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
   st->split_items = 0;
   st->runtime_tree = ctx->lastFast ? 1 : 0;
   st->waves_per_simd = ctx->lastWaves;
+  st->devices = 1;
+  st->gather = 0;
   if (ctx->d_order && ctx->orderValid) {
     int counts[NUM_QUEUES];
     CK(hipMemcpy(counts, ctx->d_order + (size_t)NUM_QUEUES * ctx->orderCap, sizeof(counts), hipMemcpyDeviceToHost));
@@ -1294,8 +1521,16 @@ int pt_fmath_device(pt_ctx* ctx, int fn, const float* x, const float* y, int n, 
   return PT_OK;
 }
 
+static int resetOne(pt_ctx* ctx);
+
 int pt_reset_stats(pt_ctx* ctx) {
   if (!ctx) return PT_E_INVALID;
+  for (pt_ctx* p : ctx->peers)
+    if (int rc = resetOne(p)) return fromPeer(ctx, p, rc);
+  return resetOne(ctx);
+}
+
+static int resetOne(pt_ctx* ctx) {
   CK(hipSetDevice(ctx->cfg.device_id));
   CK(hipStreamSynchronize(ctx->stream));
   CK(hipMemset(ctx->d_ctl + CTL_STATS, 0, CTL_BYTES - CTL_STATS));
@@ -1306,5 +1541,159 @@ int pt_reset_stats(pt_ctx* ctx) {
   ctx->msLast = 0.0f;
   return PT_OK;
 }
+
+// ------------------------------------------------------------ device groups
+static int createGroup(pt_ctx* ctx) {
+  const int n = 1 + (int)ctx->peers.size();
+  GroupGather* g = new (std::nothrow) GroupGather();
+  if (!g) return fail(ctx, PT_E_NOMEM, "group gather");
+  ctx->gather = g;
+  g->n = n;
+  std::vector<int> devs{ctx->cfg.device_id};
+  for (pt_ctx* p : ctx->peers) devs.push_back(p->cfg.device_id);
+  bool distinct = true;
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++) distinct = distinct && devs[a] != devs[b];
+  const int want = ctx->cfg.gather;
+  const Rccl& R = rccl();
+  if (want == PT_GATHER_RCCL && (!distinct || !R.ok))
+    return fail(ctx, PT_E_INVALID, distinct ? R.err : "PT_GATHER_RCCL needs distinct devices");
+  g->mode = (want == PT_GATHER_RCCL || (want == PT_GATHER_AUTO && distinct && R.ok)) ? PT_GATHER_RCCL : PT_GATHER_COPY;
+  // peer access lets hipMemcpyPeerAsync go device to device over xGMI (best effort)
+  for (int k = 1; k < n; k++)
+    if (devs[k] != devs[0]) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devs[0], devs[k]) == hipSuccess && can) {
+        (void)hipSetDevice(devs[0]);
+        (void)hipDeviceEnablePeerAccess(devs[k], 0);
+        (void)hipGetLastError();  // "already enabled" is fine
+      }
+    }
+  CK(hipSetDevice(devs[0]));
+  CK(hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking));
+  CK(hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
+  g->peer.resize(n - 1);
+  for (int k = 1; k < n; k++) {
+    GroupGather::Peer& P = g->peer[k - 1];
+    pt_ctx* m = ctx->peers[k - 1];
+    P.dev = devs[k];
+    P.count = (size_t)packParams(m, k, n).count;
+    CK(hipSetDevice(devs[0]));
+    if (P.count) CK(hipMalloc(&P.recv, P.count * sizeof(float4)));
+    // copy mode: the transfer (and its completion event) runs on rank 0's device
+    for (int i = 0; i < 2; i++)
+      if (g->mode == PT_GATHER_COPY) CK(hipEventCreateWithFlags(&P.sent[i], hipEventDisableTiming));
+    CK(hipSetDevice(P.dev));
+    for (int i = 0; i < 2; i++) {
+      if (P.count) CK(hipMalloc(&P.send[i], P.count * sizeof(float4)));
+      CK(hipEventCreateWithFlags(&P.packed[i], hipEventDisableTiming));
+      if (g->mode == PT_GATHER_RCCL) CK(hipEventCreateWithFlags(&P.sent[i], hipEventDisableTiming));
+    }
+    if (g->mode == PT_GATHER_RCCL) CK(hipStreamCreateWithFlags(&P.mstream, hipStreamNonBlocking));
+  }
+  if (g->mode == PT_GATHER_RCCL) {
+    ncclResult_t e = R.commInitAll(g->comms, n, devs.data());
+    if (e != ncclSuccess) return fail(ctx, PT_E_HIP, std::string("ncclCommInitAll: ") + R.errorString(e));
+    g->commsReady = true;
+  }
+  CK(hipSetDevice(devs[0]));
+  return PT_OK;
+}
+
+static int groupGather(pt_ctx* ctx) {
+  GroupGather& g = *ctx->gather;
+  const int i = (int)(g.frame++ & 1u);
+  const int n = g.n;
+  const int dev0 = ctx->cfg.device_id;
+  // each rank's tiles of this frame, packed on its render stream behind the frame
+  for (int k = 1; k < n; k++) {
+    GroupGather::Peer& P = g.peer[k - 1];
+    pt_ctx* m = ctx->peers[k - 1];
+    if (!P.count) continue;
+    CK(hipSetDevice(P.dev));
+    if (P.sentValid[i]) CK(hipStreamWaitEvent(m->stream, P.sent[i], 0));
+    CK(launchPack(packParams(m, k, n), m->d_accum, P.send[i], m->stream));
+    CK(hipEventRecord(P.packed[i], m->stream));
+  }
+  if (g.mode == PT_GATHER_RCCL) {
+    const Rccl& R = rccl();
+    for (auto& P : g.peer)
+      if (P.count) {
+        CK(hipSetDevice(P.dev));
+        CK(hipStreamWaitEvent(P.mstream, P.packed[i], 0));
+      }
+    ncclResult_t e = R.groupStart();
+    for (int k = 1; k < n && e == ncclSuccess; k++) {
+      GroupGather::Peer& P = g.peer[k - 1];
+      if (!P.count) continue;
+      e = R.send(P.send[i], P.count * 4, ncclFloat32, 0, g.comms[k], P.mstream);
+      if (e == ncclSuccess) e = R.recv(P.recv, P.count * 4, ncclFloat32, k, g.comms[0], g.cstream);
+    }
+    ncclResult_t e2 = R.groupEnd();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) return fail(ctx, PT_E_HIP, std::string("RCCL gather: ") + R.errorString(e));
+    for (auto& P : g.peer)
+      if (P.count) {
+        CK(hipSetDevice(P.dev));
+        CK(hipEventRecord(P.sent[i], P.mstream));
+      }
+  } else {
+    CK(hipSetDevice(dev0));
+    for (auto& P : g.peer) {
+      if (!P.count) continue;
+      CK(hipStreamWaitEvent(g.cstream, P.packed[i], 0));
+      CK(hipMemcpyPeerAsync(P.recv, dev0, P.send[i], P.dev, P.count * sizeof(float4), g.cstream));
+      CK(hipEventRecord(P.sent[i], g.cstream));
+    }
+  }
+  CK(hipSetDevice(dev0));
+  for (int k = 1; k < n; k++) {
+    GroupGather::Peer& P = g.peer[k - 1];
+    if (P.count) CK(launchUnpack(packParams(ctx, k, n), ctx->d_accum, P.recv, g.cstream));
+    P.sentValid[i] = P.count > 0;
+  }
+  CK(hipEventRecord(g.done, g.cstream));
+  g.pending = true;
+  return PT_OK;
+}
+
+static void destroyGroup(pt_ctx* ctx) {
+  GroupGather* g = ctx->gather;
+  if (g) {
+    if (g->cstream) {
+      (void)hipSetDevice(ctx->cfg.device_id);
+      (void)hipStreamSynchronize(g->cstream);
+    }
+    for (auto& P : g->peer) {
+      (void)hipSetDevice(P.dev);
+      if (P.mstream) (void)hipStreamSynchronize(P.mstream);
+    }
+    if (g->commsReady)
+      for (int k = 0; k < g->n; k++)
+        if (g->comms[k]) (void)rccl().commDestroy(g->comms[k]);
+    for (auto& P : g->peer) {
+      (void)hipSetDevice(P.dev);
+      for (int i = 0; i < 2; i++) {
+        dfree(P.send[i]);
+        if (P.packed[i]) (void)hipEventDestroy(P.packed[i]);
+        if (g->mode == PT_GATHER_RCCL && P.sent[i]) (void)hipEventDestroy(P.sent[i]);
+      }
+      if (P.mstream) (void)hipStreamDestroy(P.mstream);
+      (void)hipSetDevice(ctx->cfg.device_id);
+      dfree(P.recv);
+      for (int i = 0; i < 2; i++)
+        if (g->mode == PT_GATHER_COPY && P.sent[i]) (void)hipEventDestroy(P.sent[i]);
+    }
+    (void)hipSetDevice(ctx->cfg.device_id);
+    if (g->done) (void)hipEventDestroy(g->done);
+    if (g->cstream) (void)hipStreamDestroy(g->cstream);
+    delete g;
+    ctx->gather = nullptr;
+  }
+  for (pt_ctx* p : ctx->peers) pt_destroy(p);
+  ctx->peers.clear();
+}
+
+int pt_abi_version(void) { return PT_ABI_VERSION; }
 
 }  // extern "C"

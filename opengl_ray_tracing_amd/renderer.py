@@ -32,6 +32,7 @@ FLAG_WAVEFRONT = 0x8
 FLAG_REGEN = 0x10
 FLAG_NO_TILE_ORDER = 0x20
 FLAG_REFERENCE_TREE = 0x40
+GATHER = {"auto": 0, "copy": 1, "rccl": 2}
 
 
 @dataclass
@@ -48,6 +49,8 @@ class FrameStats:
     split_items: int
     runtime_tree: int
     waves_per_simd: int
+    devices: int = 1
+    gather: int = 0
 
 
 def _fp(a: np.ndarray):
@@ -63,7 +66,11 @@ def device_count() -> int:
 class Renderer:
     def __init__(self, width: int, height: int, integrator="lambert", max_bounce: int = -1, device: int = 0,
                  tile_rank: int = 0, tile_world: int = 1, tile_size: int = 32, flags: int = 0,
-                 basic_samples: int = 128, basic_seed: int = 0, sample_rank: int = 0, sample_world: int = 1):
+                 basic_samples: int = 128, basic_seed: int = 0, sample_rank: int = 0, sample_world: int = 1,
+                 devices=None, gather="auto"):
+        """devices: a list of HIP device ids (2..8, repeats allowed) makes this one context render
+        screen tiles on all of them and gather them into the first device's accumulation every
+        frame (pt_config.n_devices; gather "auto" / "copy" / "rccl")."""
         self._lib = _native.load()
         cfg = _native.PtConfig()
         cfg.width, cfg.height = int(width), int(height)
@@ -75,6 +82,12 @@ class Renderer:
         cfg.basic_samples = int(basic_samples)
         cfg.basic_seed = int(basic_seed) & 0xFFFFFFFF
         cfg.sample_rank, cfg.sample_world = int(sample_rank), int(sample_world)
+        if devices is not None and len(devices) > 1:
+            cfg.n_devices = len(devices)
+            for k, d in enumerate(devices):
+                cfg.device_ids[k] = int(d)
+            cfg.device_id = int(devices[0])
+        cfg.gather = GATHER[gather] if isinstance(gather, str) else int(gather)
         h = C.c_void_p()
         _native.check(self._lib.pt_create(C.byref(h), C.byref(cfg)), None, "pt_create")
         self._h = h
@@ -197,7 +210,7 @@ class Renderer:
         self._ck(self._lib.pt_get_stats(self._h, C.byref(s)), "pt_get_stats")
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
                           s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
-                          s.waves_per_simd)
+                          s.waves_per_simd, s.devices, s.gather)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

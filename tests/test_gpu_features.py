@@ -274,3 +274,38 @@ def test_launch_timing_ring_keeps_stats_exact():
         st = r.stats()
         assert st.launches == frames and st.kernel_ms_total > 0
         assert st.rays >= frames * 64 * 36
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_device_group_equals_one_device(devices):
+    """One context over several devices (pt_config.n_devices; on the one-GPU box the same
+    device repeated, so the gather runs as peer copies): every device renders its screen
+    tiles and each frame gathers them into the first device's accumulation. The image equals
+    a one-device render bit for bit across frames and a camera reset, with the same rays."""
+    cfg, tris, nodes, hdr = scenes.build_config("c2")
+    w, h = 480, 270
+    eye, rot = orbit_camera(*cfg.camera)
+    eye2, rot2 = orbit_camera(20.0, 10.0, 4.0)
+    cams = [(eye, rot, f) for f in range(3)] + [(eye2, rot2, f) for f in range(2)]  # reset at frame 3
+
+    def run(**kw):
+        with Renderer(w, h, "lambert", **kw) as r:
+            r.upload_scene(tris, nodes)
+            r.upload_env(hdr)
+            imgs = []
+            for e, m, f in cams:
+                r.render_frame(e, m, f, sync=False)
+                if f == 2:
+                    imgs.append(r.accum())
+            imgs.append(r.accum())
+            return imgs, r.tonemap(1.5), r.stats()
+
+    ref, ref_tm, ref_st = run()
+    got, got_tm, st = run(devices=devices)
+    assert st.devices == len(devices) and st.gather == 1  # PT_GATHER_COPY: the ids repeat
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+    assert np.array_equal(got_tm, ref_tm)
+    assert st.rays == ref_st.rays
+    with pytest.raises(_native.PtError):  # RCCL needs distinct devices
+        Renderer(w, h, "lambert", devices=devices, gather="rccl")
