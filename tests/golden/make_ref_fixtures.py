@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Make tests/golden/ref/ from the reference's own host code (TEST INFRASTRUCTURE).
+
+Builds oracle/_ref/ref_harness (oracle/ref_build.py: the reference's readObj,
+getTransformMatrix, buildBVHwithSAH, buildBVH and calculateHdrCache compiled
+from /root/reference) and runs it on the inputs of tests/ref_scenes.py:
+
+  ref/<scene>_<builder>.json   sha256 of the Triangle_encoded and BVHNode_encoded
+                               arrays main() would upload, their shapes, and the
+                               node array itself (n x 12 float32, zlib + base64)
+  ref/hdrcache_<env>.json      sha256 of calculateHdrCache's output for the
+                               repository's decode of the shipped .hdr, and 4096
+                               sampled texels of it
+
+    python tests/golden/make_ref_fixtures.py
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import json
+import zlib
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+import ref_build  # noqa: E402
+import ref_scenes  # noqa: E402
+from opengl_ray_tracing_amd import scenes  # noqa: E402
+
+OUT = Path(__file__).resolve().parent / "ref"
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def pack(a: np.ndarray) -> str:
+    """float32 array -> base64(zlib(bytes)) (tests/test_ref_pinned.py unpacks it)."""
+    return base64.b64encode(zlib.compress(np.ascontiguousarray(a, np.float32).tobytes(), 9)).decode()
+
+
+def run_scene(exe: Path, name: str, builder: str, tmp: Path):
+    lines = []
+    for k, (text, mat, (r, t, s), smooth) in enumerate(ref_scenes.parts(name)):
+        obj = tmp / f"{name}_{k}.obj"
+        obj.write_text(text)
+        nums = [*r, *t, *s, *ref_scenes.material_floats(mat)]
+        lines.append(f"{obj} {int(smooth)} " + " ".join(f"{float(np.float32(x)):.9g}" for x in nums))
+    spec = tmp / f"{name}.spec"
+    spec.write_text("\n".join(lines) + "\n")
+    tp, np_ = tmp / "tris.f32", tmp / "nodes.f32"
+    subprocess.run([str(exe), "scene", str(spec), builder, str(tp), str(np_)], check=True)
+    tris = np.fromfile(tp, np.float32).reshape(-1, 36)
+    nodes = np.fromfile(np_, np.float32).reshape(-1, 12)
+    return tris, nodes
+
+
+def main():
+    exe = ref_build.build()
+    if exe is None:
+        raise SystemExit("the reference is not present: fixtures cannot be regenerated here")
+    OUT.mkdir(exist_ok=True)
+    with tempfile.TemporaryDirectory() as d:
+        tmp = Path(d)
+        for name, builder in ref_scenes.BUILDS:
+            if len(sys.argv) > 1 and name not in sys.argv[1:]:
+                continue
+            tris, nodes = run_scene(exe, name, builder, tmp)
+            ent = {"scene": name, "builder": builder, "generator": "oracle/ref_harness (reference main.cpp code)",
+                   "tris_shape": list(tris.shape), "tris_sha256": sha(tris)}
+            if builder != "none":
+                ent.update(nodes_shape=list(nodes.shape), nodes_sha256=sha(nodes))
+                if name not in ref_scenes.BIG:
+                    ent["nodes_f32_zlib_b64"] = pack(nodes)
+            else:
+                ent["tris_f32_zlib_b64"] = pack(tris)
+            (OUT / f"{name}_{builder}.json").write_text(json.dumps(ent) + "\n")
+            print(name, builder, tris.shape, nodes.shape)
+        for env in ref_scenes.HDRS if len(sys.argv) == 1 else ():
+            hdr = np.ascontiguousarray(scenes.load_hdr(scenes.HDR_FILES[env]), np.float32)
+            h, w = hdr.shape[:2]
+            hp, cp = tmp / "hdr.f32", tmp / "cache.f32"
+            hdr.tofile(hp)
+            subprocess.run([str(exe), "hdrcache", str(hp), str(w), str(h), str(cp)], check=True)
+            cache = np.fromfile(cp, np.float32).reshape(h, w, 3)
+            rng = np.random.default_rng(11)
+            idx = rng.choice(h * w, 4096, replace=False)
+            ent = {"env": env, "width": w, "height": h, "hdr_sha256": sha(hdr), "cache_sha256": sha(cache),
+                   "sample_index": idx.tolist(), "sample_values": cache.reshape(-1, 3)[idx].tolist(),
+                   "generator": "oracle/ref_harness (reference calculateHdrCache)"}
+            (OUT / f"hdrcache_{env}.json").write_text(json.dumps(ent) + "\n")
+            print(env, w, h)
+
+
+if __name__ == "__main__":
+    main()
