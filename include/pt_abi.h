@@ -52,6 +52,7 @@ extern "C" {
 #define PT_FLAG_REGEN 0x10u       /* path-regeneration state-machine kernel instead of the megakernel */
 #define PT_FLAG_NO_TILE_ORDER 0x20u /* megakernel: hand out tiles in fixed order, not longest-first */
 #define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */
+#define PT_FLAG_SERIAL_FRAMES 0x80u /* megakernel: no frames in flight (each frame starts after the previous one ends) */
 
 /* in-process multi-GPU (pt_config.n_devices > 1) */
 #define PT_MAX_DEVICES 8
@@ -104,6 +105,8 @@ typedef struct pt_frame_stats {
                            (3 = the large-scene Disney/MIS variant, else its default bound) */
   int devices;          /* devices the context renders on (1, or pt_config.n_devices) */
   int gather;           /* PT_GATHER_COPY / PT_GATHER_RCCL in use (0 with one device) */
+  int frames_in_flight; /* megakernel frames that may overlap (1 = serial; >1: kernel_ms of
+                           overlapping launches add up to more than the wall time) */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;

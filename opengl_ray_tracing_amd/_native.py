@@ -34,7 +34,7 @@ class PtFrameStats(C.Structure):
         ("mat_fetch", C.c_uint64), ("tex_fetch", C.c_uint64), ("kernel_ms", C.c_float),
         ("kernel_ms_total", C.c_float), ("launches", C.c_int), ("max_stack", C.c_int),
         ("split_items", C.c_int), ("runtime_tree", C.c_int),
-        ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int),
+        ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int), ("frames_in_flight", C.c_int),
     ]
 
 

@@ -126,6 +126,10 @@ struct RenderParams {
   float eye[3];
   float cam[16];
   float4* accum;
+  // Pipelined frames (pt_runtime.cpp "frames in flight"): non-null = write each pixel's
+  // sample colour here (float4, w unused) and leave the running mean to mixKernel, which
+  // runs in frame order; null = mix into accum in place (IS:868-871)
+  float4* col;
   int* queue;           // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
   int perQueue;         // items per queue
   int numItems;         // 8x8 wave tiles owned by this rank
@@ -196,5 +200,8 @@ hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, fl
 hipError_t launchPack(const PackParams& p, const float4* accum, float4* packed, hipStream_t s);
 hipError_t launchFmath(int fn, const float* x, const float* y, int n, float* out, hipStream_t s);
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float4* packed, hipStream_t s);
+// the running-mean update of a pipelined frame over the rank's owned pixels (PackParams
+// mapping): accum = mix(accum, col, 1 / (frameCounter + 1)) (IS:868-871, pass2.fsh:15)
+hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s);
 
 }  // namespace pt

@@ -219,6 +219,10 @@ __device__ __forceinline__ V3 cameraRay(const RenderParams& p, int px, int py, u
 }
 
 __device__ __forceinline__ void accumulate(const RenderParams& p, int px, int py, V3 color, Counters& C, bool count) {
+  if (!count && p.col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in order
+    stStream(p.col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
+    return;
+  }
   float4* a = p.accum + (size_t)py * p.width + px;
   float4 old = ldStream(a);
   if (count) C.texels++;
@@ -756,6 +760,19 @@ __global__ void unpackKernel(PackParams p, float4* accum, const float4* packed) 
   if (packedPixel(p, k, px, py)) accum[(size_t)py * p.width + px] = packed[k];
 }
 
+// the running mean of a pipelined frame (accumulate's update, deferred to frame order)
+__global__ void mixKernel(PackParams p, float4* accum, const float4* col, uint32_t frameCounter) {
+  long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= p.count) return;
+  int px, py;
+  if (!packedPixel(p, k, px, py)) return;
+  const size_t i = (size_t)py * p.width + px;
+  const float4 c = ldStream(col + i);
+  const float4 old = ldStream(accum + i);
+  const float w = 1.0f / (float)(frameCounter + 1u);
+  stStream(accum + i, make_float4(mixf(old.x, c.x, w), mixf(old.y, c.y, w), mixf(old.z, c.z, w), 1.0f));
+}
+
 // include/pt_fmath.h evaluated on the device (diagnostics; bit-equality with the host)
 __device__ __forceinline__ float fmathEval(int fn, float x, float y) {
   switch (fn) {
@@ -841,6 +858,11 @@ hipError_t launchFmath(int fn, const float* x, const float* y, int n, float* out
 hipError_t launchPack(const PackParams& p, const float4* accum, float4* packed, hipStream_t s) {
   if (p.count <= 0) return hipSuccess;
   hipLaunchKernelGGL(packKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, packed);
+  return hipGetLastError();
+}
+hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s) {
+  if (p.count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, col, frameCounter);
   return hipGetLastError();
 }
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float4* packed, hipStream_t s) {

@@ -26,6 +26,15 @@
 using namespace pt;
 
 static constexpr int EV_RING = 64;
+// Frames in flight: the default megakernel's frame f runs on slot stream f % PIPE
+// with its own work queues, overflow stack, tile order and colour buffer, so
+// frame f+1 can fill the SIMDs that frame f's last long paths leave idle. Each
+// frame's running-mean update (mixKernel) waits for the previous frame's, so the
+// accumulation is updated in frame order and the image is bit for bit the one
+// of serial frames (c4: two overlapped frames measured 1.57x the throughput of
+// serial ones, tools/overlap_probe.py).
+static constexpr int PIPE = 2;
+static_assert(PIPE * NUM_QUEUES * CTL_LINE_INTS * 4 <= (int)CTL_STATS, "queue counters of every slot fit the control block");
 
 #ifndef PT_TILE_GROUP
 #define PT_TILE_GROUP 1  // tiles ordered by cost in groups of this many consecutive tiles (1 measured best)
@@ -82,20 +91,29 @@ struct pt_ctx {
   // launch), cumulative fetch stats, padded sharded cumulative ray counters
   unsigned char* d_ctl = nullptr;
   int* d_ovf = nullptr;
-  int* d_cost = nullptr;   // per-tile cost of the last frame (megakernel)
-  int* d_order = nullptr;  // per-band tile order for the next frame
+  int* d_cost = nullptr;   // per slot: per-tile cost of its last frame, longest item, split state, estimate
+  int* d_order = nullptr;  // per slot: per-band work items for its next frame
   bool lastFast = false;    // the last megakernel frame traversed the runtime's tree
   int lastWaves = 0;        // waves per SIMD of the last megakernel launch (occupancy query)
   // tree / tile-split policy probe (probePolicy): frames since the probe (re)started,
   // the summed frame times of each policy, the decision
   int probeFrame = 0;
+  // frames in flight (PIPE slots; see PIPE above)
+  bool pipe = false;                        // this context pipelines its megakernel frames
+  hipStream_t slotStream[PIPE] = {};
+  hipEvent_t mixDone[PIPE] = {};            // slot's last running-mean update
+  hipEvent_t userMark = nullptr;            // the caller's stream at the last frame's call
+  float4* d_col[PIPE] = {};                 // per-slot sample colours
+  int lastSlot = -1;                        // slot of the last pipelined frame
+  bool mixPending = false;                  // a pipelined frame's update may still be running
+  unsigned long long frameNo = 0;           // pipelined frames issued
   int probeN[3] = {0, 0, 0};           // timed frames: runtime tree, uploaded tree (both unsplit), split
   double probeMs[3] = {0.0, 0.0, 0.0};
   long long probeLast[3] = {-1, -1, -1};  // launch number of each slot's last timed frame
   int probeGen = 0;
   int treeDecided = -1, splitDecided = -1;  // -1 probing, 0 off, 1 on
   int orderCap = 0;        // work items per band in d_order
-  bool orderValid = false;
+  bool orderValid[PIPE] = {};
   size_t ovfInts = 0;
   // shards
   int shardSize = 32, shardsX = 0, shardsY = 0, numItems = 0, perQueue = 0;
@@ -252,6 +270,17 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   const int owned = (numShards - cfg->tile_rank + cfg->tile_world - 1) / cfg->tile_world;
   ctx->numItems = owned * (ss / 8) * (ss / 8);
   ctx->perQueue = (ctx->numItems + NUM_QUEUES - 1) / NUM_QUEUES;
+  // the default megakernel pipelines its frames (not BASIC, the fetch counter, the
+  // wavefront / regeneration kernels or PT_FLAG_SERIAL_FRAMES)
+  ctx->pipe = cfg->integrator != PT_BASIC_CPU_COMPAT &&
+              !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_WAVEFRONT | PT_FLAG_REGEN | PT_FLAG_SERIAL_FRAMES));
+  if (ctx->pipe) {
+    CKC(hipEventCreateWithFlags(&ctx->userMark, hipEventDisableTiming));
+    for (int k = 0; k < PIPE; k++) {
+      CKC(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
+      CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
+    }
+  }
 #undef CKC
   *out = ctx;
   return PT_OK;
@@ -315,6 +344,13 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
+  for (int k = 0; k < PIPE; k++) {
+    if (ctx->slotStream[k]) (void)hipStreamSynchronize(ctx->slotStream[k]);
+    dfree(ctx->d_col[k]);
+    if (ctx->mixDone[k]) (void)hipEventDestroy(ctx->mixDone[k]);
+    if (ctx->slotStream[k]) (void)hipStreamDestroy(ctx->slotStream[k]);
+  }
+  if (ctx->userMark) (void)hipEventDestroy(ctx->userMark);
   freeWavefront(ctx);
   for (hipEvent_t e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -640,7 +676,10 @@ static std::string prepareScene(const float* tris, int nTri, const float* nodes,
   return "";
 }
 
+static int syncStreams(pt_ctx* ctx);
+
 static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
+  if (int rc = syncStreams(ctx)) return rc;  // no frame in flight reads the buffers replaced here
   CK(hipSetDevice(ctx->cfg.device_id));
   int rc;
   if ((rc = upload(ctx, &ctx->d_pairs, h.pairs)) || (rc = upload(ctx, &ctx->d_geo, h.geo)) ||
@@ -715,6 +754,7 @@ static int deviceHdrCache(pt_ctx* ctx, const float* hdr, int w, int h, float4* o
 
 static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache) {
   if (!ctx) return PT_E_INVALID;
+  if (int rc = syncStreams(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   dfree(ctx->d_hdr);
   dfree(ctx->d_cache);
@@ -888,11 +928,11 @@ static SceneView sceneView(const pt_ctx* ctx) {
 }
 
 // make sure the overflow stack covers `threads` threads of a kernel keeping `ldsDepth` entries in LDS
-static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDepth = LDS_STACK) {
+static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDepth = LDS_STACK, int slots = 1) {
   // pt_trace.h StackT: at most maxStack - ldsDepth/2 - 1 entries are ever in HBM
   *ovfDepth = ctx->maxStack > ldsDepth ? ctx->maxStack - ldsDepth / 2 : 0;
   if (*ovfDepth == 0) return PT_OK;
-  size_t need = threads * (size_t)(*ovfDepth);
+  size_t need = threads * (size_t)(*ovfDepth) * (size_t)slots;  // slots: one region per frame in flight
   if (need > ctx->ovfInts) {
     dfree(ctx->d_ovf);
     CK(hipMalloc(&ctx->d_ovf, need * sizeof(int)));
@@ -1056,9 +1096,12 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
       ctx->probeLast[k] = -1;
     }
     ctx->treeDecided = ctx->splitDecided = -1;
-    // split state and cost estimates start over (the camera or scene changed)
-    if (ctx->d_cost) (void)hipMemsetAsync(ctx->d_cost + 2 * (size_t)ctx->numItems, 0,
-                                          2 * (size_t)ctx->numItems * sizeof(int), ctx->stream);
+    // split state and cost estimates start over (the camera or scene changed), in
+    // every slot's stream order (after its last reorder, before its next frame)
+    if (ctx->d_cost)
+      for (int k = 0; k < (ctx->pipe ? PIPE : 1); k++)
+        (void)hipMemsetAsync(ctx->d_cost + (size_t)k * 4 * ctx->numItems + 2 * (size_t)ctx->numItems, 0,
+                             2 * (size_t)ctx->numItems * sizeof(int), ctx->pipe ? ctx->slotStream[k] : ctx->stream);
   }
   const int f = ctx->probeFrame < 1000 ? ctx->probeFrame++ : 1000;
   auto avg = [&](int k) { return ctx->probeN[k] ? ctx->probeMs[k] / ctx->probeN[k] : 1e30; };
@@ -1083,17 +1126,18 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
   return f >= 6 ? PT_SPLIT_PCT : 0;
 }
 
+static PackParams packParams(const pt_ctx* ctx, int rank, int world);
+
 static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
   if (!ctx) return PT_E_INVALID;
   CK(hipSetDevice(ctx->cfg.device_id));
   const pt_config& c = ctx->cfg;
   unsigned long long* stats = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_STATS);
-  CK(hipMemsetAsync(ctx->d_ctl + CTL_QUEUES, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), ctx->stream));
   hipEvent_t evb, eve;
-  int erc = launchEvents(ctx, &evb, &eve);
-  if (erc) return erc;
   if (c.integrator == PT_BASIC_CPU_COMPAT) {
     if (!ctx->d_shapes) return fail(ctx, PT_E_NOSCENE, "no BASIC shapes uploaded");
+    int erc = launchEvents(ctx, &evb, &eve);
+    if (erc) return erc;
     BasicParams p;
     p.shapes = ctx->d_shapes;
     p.nShapes = ctx->nShapes;
@@ -1114,11 +1158,19 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (!ctx->d_bvh || !eye || !cameraRotate) return fail(ctx, ctx->d_bvh ? PT_E_INVALID : PT_E_NOSCENE, "no scene");
   const bool count = (c.flags & PT_FLAG_COUNT_FETCHES) != 0;
   const bool cull = !count && !(c.flags & PT_FLAG_NO_CULL);
-  if (!count && (c.flags & PT_FLAG_WAVEFRONT))
+  if (!count && (c.flags & PT_FLAG_WAVEFRONT)) {
+    CK(hipMemsetAsync(ctx->d_ctl + CTL_QUEUES, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), ctx->stream));
+    int erc = launchEvents(ctx, &evb, &eve);
+    if (erc) return erc;
     return renderWavefront(ctx, eye, cameraRotate, frameCounter, cull, stats, evb, eve);
+  }
   // default: the lock-step persistent megakernel (also the fetch-counting
   // variant); the path-regeneration kernel on request
   const bool regen = !count && (c.flags & PT_FLAG_REGEN);
+  // this frame's stream and per-frame buffers: slot frameNo % PIPE when pipelined
+  const bool piped = ctx->pipe && !regen && !count;
+  const int slot = piped ? (int)(ctx->frameNo % PIPE) : 0;
+  hipStream_t S = piped ? ctx->slotStream[slot] : ctx->stream;
   int nb = 0;
   if (regen) CK(regenBlocksPerCU(c.integrator, cull, &nb));
   // large scenes: the more-waves variant (pt_kernels.h PT_WIDE_SCENE_MB)
@@ -1129,8 +1181,12 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   ctx->lastWaves = regen ? 0 : nb * BLOCK / 64 / 4;  // 4 SIMDs per CU
   int grid = ctx->numCU * nb;
   int ovfDepth = 0;
-  int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK);
+  int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, piped ? PIPE : 1);
   if (rc) return rc;
+  const size_t npix = (size_t)c.width * c.height;
+  if (piped && !ctx->d_col[slot]) CK(hipMalloc(&ctx->d_col[slot], npix * sizeof(float4)));
+  int* queue = reinterpret_cast<int*>(ctx->d_ctl + CTL_QUEUES) + (size_t)slot * NUM_QUEUES * CTL_LINE_INTS;
+  CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   RenderParams p;
   std::memset(&p, 0, sizeof(p));
   p.scene = sceneView(ctx);
@@ -1147,7 +1203,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   std::memcpy(p.eye, eye, sizeof(p.eye));
   std::memcpy(p.cam, cameraRotate, sizeof(p.cam));
   p.accum = ctx->d_accum;
-  p.queue = reinterpret_cast<int*>(ctx->d_ctl);
+  p.col = piped ? ctx->d_col[slot] : nullptr;
+  p.queue = queue;
   p.perQueue = ctx->perQueue;
   p.numItems = ctx->numItems;
   p.shardSize = ctx->shardSize;
@@ -1155,7 +1212,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.shardsX = ctx->shardsX;
   p.rank = c.tile_rank;
   p.world = c.tile_world;
-  p.ovf = ovfDepth ? ctx->d_ovf : nullptr;
+  p.ovf = ovfDepth ? ctx->d_ovf + (size_t)slot * grid * BLOCK * ovfDepth : nullptr;
   p.ovfDepth = ovfDepth;
   p.scene.fast = 0;  // probePolicy below
 
@@ -1166,15 +1223,20 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const bool ordered = !regen && !count && !(c.flags & PT_FLAG_NO_TILE_ORDER) &&
                        (ctx->perQueue + group - 1) / group <= REORDER_MAX && ctx->numItems < (1 << 22);
   const int orderCap = 4 * ctx->perQueue + 64;  // room for the items of split tiles
+  const size_t orderInts = (size_t)NUM_QUEUES * orderCap + NUM_QUEUES;
   ctx->orderCap = orderCap;
   if (ordered && !ctx->d_cost) {
-    // per tile: summed item cost, longest item, split state (reorderKernel reads and zeroes the costs)
-    CK(hipMalloc(&ctx->d_cost, (size_t)ctx->numItems * 4 * sizeof(int)));
-    CK(hipMemsetAsync(ctx->d_cost, 0, (size_t)ctx->numItems * 4 * sizeof(int), ctx->stream));
-    // per band: orderCap work items, then the NUM_QUEUES item counts (reorderKernel)
-    CK(hipMalloc(&ctx->d_order, ((size_t)NUM_QUEUES * orderCap + NUM_QUEUES) * sizeof(int)));
-    ctx->orderValid = false;
+    // per slot and tile: summed item cost, longest item, split state, cost estimate
+    // (reorderKernel reads and zeroes the costs)
+    const size_t n = (size_t)PIPE * ctx->numItems * 4;
+    CK(hipMalloc(&ctx->d_cost, n * sizeof(int)));
+    CK(hipMemset(ctx->d_cost, 0, n * sizeof(int)));
+    // per slot and band: orderCap work items, then the NUM_QUEUES item counts (reorderKernel)
+    CK(hipMalloc(&ctx->d_order, (size_t)PIPE * orderInts * sizeof(int)));
+    for (int k = 0; k < PIPE; k++) ctx->orderValid[k] = false;
   }
+  int* cost = ordered ? ctx->d_cost + (size_t)slot * 4 * ctx->numItems : nullptr;
+  int* order = ordered ? ctx->d_order + (size_t)slot * orderInts : nullptr;
   // the tree (the runtime's own, checked against the uploaded one, unless asked
   // not to) and the split policy: probePolicy
   bool useFast = false;
@@ -1183,10 +1245,16 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
-  p.tileOrder = ordered && ctx->orderValid ? ctx->d_order : nullptr;
+  p.tileOrder = ordered && ctx->orderValid[slot] ? order : nullptr;
   p.orderCap = orderCap;
-  p.tileCost = ordered ? ctx->d_cost : nullptr;
-  p.tileCostMax = ordered ? ctx->d_cost + ctx->numItems : nullptr;
+  p.tileCost = cost;
+  p.tileCostMax = ordered ? cost + ctx->numItems : nullptr;
+  // While the policy probe times frames (PT_SPLIT_AUTO, 14 frames after a restart)
+  // a pipelined frame still starts only after the previous one has ended.
+  const bool probing = ordered && PT_SPLIT_AUTO && (ctx->treeDecided < 0 || ctx->splitDecided < 0);
+  if (piped && probing && ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
+  int erc = launchEvents(ctx, &evb, &eve);
+  if (erc) return erc;
 #if PT_WAVE_TRACE
   // diagnostics build: each wave's {start, end, tiles | longest tile's pixel << 32,
   // longest tile's duration, its most node-loop / leaf-loop iterations of a lane} (100 MHz wall
@@ -1195,18 +1263,18 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   unsigned long long* dTrace = nullptr;
   if (!regen) {
     CK(hipMalloc(&dTrace, nTrace * sizeof(unsigned long long)));
-    CK(hipMemsetAsync(dTrace, 0, nTrace * sizeof(unsigned long long), ctx->stream));
+    CK(hipMemsetAsync(dTrace, 0, nTrace * sizeof(unsigned long long), S));
   }
   p.waveTrace = dTrace;
 #endif
-  CK(hipEventRecord(evb, ctx->stream));
-  if (regen) CK(launchRegen(p, c.integrator, grid, ctx->stream, cull));
-  else CK(launchRender(p, c.integrator, grid, ctx->stream, cull, count, wide));
+  CK(hipEventRecord(evb, S));
+  if (regen) CK(launchRegen(p, c.integrator, grid, S, cull));
+  else CK(launchRender(p, c.integrator, grid, S, cull, count, wide));
 #if PT_WAVE_TRACE
   if (dTrace) {
     std::vector<unsigned long long> tr(nTrace);
-    CK(hipMemcpyAsync(tr.data(), dTrace, nTrace * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
-    CK(hipStreamSynchronize(ctx->stream));
+    CK(hipMemcpyAsync(tr.data(), dTrace, nTrace * sizeof(unsigned long long), hipMemcpyDeviceToHost, S));
+    CK(hipStreamSynchronize(S));
     (void)hipFree(dTrace);
     if (const char* fn = std::getenv("PT_WAVE_TRACE_FILE")) {
       if (FILE* f = std::fopen(fn, "ab")) {
@@ -1216,14 +1284,43 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     }
   }
 #endif
-  CK(hipEventRecord(eve, ctx->stream));  // kernel_ms: the frame kernel alone (the reorder below is in the frame's wall time)
+  CK(hipEventRecord(eve, S));  // kernel_ms: the frame kernel alone (the reorder below is in the frame's wall time)
   if (ordered) {
-    CK(launchReorder(ctx->d_cost, ctx->d_cost + ctx->numItems, ctx->d_cost + 2 * (size_t)ctx->numItems,
-                     ctx->d_cost + 3 * (size_t)ctx->numItems, ctx->d_order,
-                     ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, ctx->stream));
-    ctx->orderValid = true;
+    CK(launchReorder(cost, cost + ctx->numItems, cost + 2 * (size_t)ctx->numItems, cost + 3 * (size_t)ctx->numItems,
+                     order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, S));
+    ctx->orderValid[slot] = true;
+  }
+  if (piped) {
+    // the running-mean update, in frame order: after the previous frame's update and
+    // after whatever the caller's stream held when this frame was requested
+    CK(hipEventRecord(ctx->userMark, ctx->stream));
+    CK(hipStreamWaitEvent(S, ctx->userMark, 0));
+    if (ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
+    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[slot], frameCounter, S));
+    CK(hipEventRecord(ctx->mixDone[slot], S));
+    ctx->lastSlot = slot;
+    ctx->mixPending = true;
+    ctx->frameNo++;
   }
   commitLaunch(ctx);
+  return PT_OK;
+}
+
+// the caller's stream waits for the last pipelined frame's running-mean update
+static int joinPipe(pt_ctx* ctx) {
+  if (!ctx->mixPending) return PT_OK;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastSlot], 0));
+  return PT_OK;
+}
+
+// every stream the context renders on, then its own: all work done
+static int syncStreams(pt_ctx* ctx) {
+  CK(hipSetDevice(ctx->cfg.device_id));
+  for (int k = 0; k < PIPE; k++)
+    if (ctx->slotStream[k]) CK(hipStreamSynchronize(ctx->slotStream[k]));
+  CK(hipStreamSynchronize(ctx->stream));
+  ctx->mixPending = false;
   return PT_OK;
 }
 
@@ -1293,6 +1390,7 @@ static int joinGather(pt_ctx* ctx) {
 int pt_download_accum(pt_ctx* ctx, float* accum) {
   if (!ctx || !accum) return PT_E_INVALID;
   if (int rc = joinGather(ctx)) return rc;
+  if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
   CK(hipMemcpyAsync(accum, ctx->d_accum, bytes, hipMemcpyDefault, ctx->stream));  // host or device
@@ -1301,6 +1399,7 @@ int pt_download_accum(pt_ctx* ctx, float* accum) {
 }
 
 static int uploadAccumOne(pt_ctx* ctx, const float* accum) {
+  if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
   CK(hipMemcpyAsync(ctx->d_accum, accum, bytes, hipMemcpyDefault, ctx->stream));  // host or device
@@ -1321,6 +1420,7 @@ int pt_clear_accum(pt_ctx* ctx) {
   if (!ctx) return PT_E_INVALID;
   if (int rc = joinGather(ctx)) return rc;
   for (pt_ctx* m : members(ctx)) {
+    if (int rc = joinPipe(m)) return fromPeer(ctx, m, rc);
     if (hipSetDevice(m->cfg.device_id) != hipSuccess ||
         hipMemsetAsync(m->d_accum, 0, (size_t)m->cfg.width * m->cfg.height * sizeof(float4), m->stream) != hipSuccess)
       return fail(ctx, PT_E_HIP, "pt_clear_accum on device " + std::to_string(m->cfg.device_id));
@@ -1337,6 +1437,7 @@ int pt_accum_device_ptr(pt_ctx* ctx, void** dptr) {
 int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out) {
   if (!ctx || !rgb_out || !(limit > 0.0f)) return PT_E_INVALID;
   if (int rc = joinGather(ctx)) return rc;
+  if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   const int n = ctx->cfg.width * ctx->cfg.height;
   if (!ctx->d_rgb) CK(hipMalloc(&ctx->d_rgb, (size_t)n * 3 * sizeof(float)));
@@ -1370,6 +1471,7 @@ int pt_owned_pixel_count(pt_ctx* ctx, int rank, int world, int64_t* count) {
 int pt_pack_owned(pt_ctx* ctx, void* dpacked) {
   if (!ctx || !dpacked) return PT_E_INVALID;
   if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
+  if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   PackParams p = packParams(ctx, ctx->cfg.tile_rank, ctx->cfg.tile_world);
   CK(launchPack(p, ctx->d_accum, reinterpret_cast<float4*>(dpacked), ctx->stream));
@@ -1379,6 +1481,7 @@ int pt_pack_owned(pt_ctx* ctx, void* dpacked) {
 int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked) {
   if (!ctx || !dpacked || world < 1 || rank < 0 || rank >= world) return PT_E_INVALID;
   if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
+  if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   PackParams p = packParams(ctx, rank, world);
   CK(launchUnpack(p, ctx->d_accum, reinterpret_cast<const float4*>(dpacked), ctx->stream));
@@ -1391,11 +1494,7 @@ int pt_set_stream(pt_ctx* ctx, void* s) {
   return PT_OK;
 }
 
-static int syncOne(pt_ctx* ctx) {
-  CK(hipSetDevice(ctx->cfg.device_id));
-  CK(hipStreamSynchronize(ctx->stream));
-  return PT_OK;
-}
+static int syncOne(pt_ctx* ctx) { return syncStreams(ctx); }
 
 // a group: every device's render stream, the gather's streams, then rank 0's stream
 static int syncGroup(pt_ctx* ctx) {
@@ -1447,8 +1546,7 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
 }
 
 static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
-  CK(hipSetDevice(ctx->cfg.device_id));
-  CK(hipStreamSynchronize(ctx->stream));
+  if (int rc = syncStreams(ctx)) return rc;
   unsigned long long h[5];
   std::vector<unsigned long long> shards((size_t)RAY_SHARDS * RAY_SHARD_STRIDE);
   CK(hipMemcpy(h, ctx->d_ctl + CTL_STATS, sizeof(h), hipMemcpyDeviceToHost));
@@ -1472,9 +1570,12 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->waves_per_simd = ctx->lastWaves;
   st->devices = 1;
   st->gather = 0;
-  if (ctx->d_order && ctx->orderValid) {
+  st->frames_in_flight = ctx->pipe ? PIPE : 1;
+  const int ls = ctx->pipe && ctx->frameNo > 0 ? (int)((ctx->frameNo - 1) % PIPE) : 0;  // the last frame's slot
+  if (ctx->d_order && ctx->orderValid[ls]) {
     int counts[NUM_QUEUES];
-    CK(hipMemcpy(counts, ctx->d_order + (size_t)NUM_QUEUES * ctx->orderCap, sizeof(counts), hipMemcpyDeviceToHost));
+    const int* ord = ctx->d_order + (size_t)ls * ((size_t)NUM_QUEUES * ctx->orderCap + NUM_QUEUES);
+    CK(hipMemcpy(counts, ord + (size_t)NUM_QUEUES * ctx->orderCap, sizeof(counts), hipMemcpyDeviceToHost));
     long items = 0;
     for (int q = 0; q < NUM_QUEUES; q++) items += counts[q];
     st->split_items = (int)std::max(0L, items - (long)ctx->numItems);
@@ -1531,8 +1632,7 @@ int pt_reset_stats(pt_ctx* ctx) {
 }
 
 static int resetOne(pt_ctx* ctx) {
-  CK(hipSetDevice(ctx->cfg.device_id));
-  CK(hipStreamSynchronize(ctx->stream));
+  if (int rc = syncStreams(ctx)) return rc;
   CK(hipMemset(ctx->d_ctl + CTL_STATS, 0, CTL_BYTES - CTL_STATS));
   while (foldOne(ctx, true)) {
   }
@@ -1610,6 +1710,7 @@ static int groupGather(pt_ctx* ctx) {
     GroupGather::Peer& P = g.peer[k - 1];
     pt_ctx* m = ctx->peers[k - 1];
     if (!P.count) continue;
+    if (int rc = joinPipe(m)) return fromPeer(ctx, m, rc);
     CK(hipSetDevice(P.dev));
     if (P.sentValid[i]) CK(hipStreamWaitEvent(m->stream, P.sent[i], 0));
     CK(launchPack(packParams(m, k, n), m->d_accum, P.send[i], m->stream));

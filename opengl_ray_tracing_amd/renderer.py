@@ -32,6 +32,7 @@ FLAG_WAVEFRONT = 0x8
 FLAG_REGEN = 0x10
 FLAG_NO_TILE_ORDER = 0x20
 FLAG_REFERENCE_TREE = 0x40
+FLAG_SERIAL_FRAMES = 0x80
 GATHER = {"auto": 0, "copy": 1, "rccl": 2}
 
 
@@ -51,6 +52,7 @@ class FrameStats:
     waves_per_simd: int
     devices: int = 1
     gather: int = 0
+    frames_in_flight: int = 1
 
 
 def _fp(a: np.ndarray):
@@ -210,7 +212,7 @@ class Renderer:
         self._ck(self._lib.pt_get_stats(self._h, C.byref(s)), "pt_get_stats")
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
                           s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
-                          s.waves_per_simd, s.devices, s.gather)
+                          s.waves_per_simd, s.devices, s.gather, s.frames_in_flight)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

@@ -232,3 +232,37 @@ def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
     o, _ = render_oracle(cfg, tris, nodes, hdr, px, frames=2, max_bounce=mb, w=w, h=h)
     parity.assert_parity(g[px[:, 1], px[:, 0]], o[px[:, 1], px[:, 0]], "wide/mis")
     assert np.all(g[..., 3] == 1.0)
+
+
+@pytest.mark.parametrize("name,tile", [("c4", (0, 1)), ("c2", (1, 3))])
+def test_pipelined_frames_equal_serial_frames(request, name, tile):
+    """Frames in flight (the default: frame f+1's megakernel overlaps frame f's tail, each
+    frame's running-mean update runs in frame order) give the image of serial frames
+    (PT_FLAG_SERIAL_FRAMES) bit for bit -- through the policy probe, a camera reset, images
+    read mid-stream and a screen-tile shard -- with the same rays."""
+    from opengl_ray_tracing_amd import FLAG_SERIAL_FRAMES
+    cfg, tris, nodes, hdr = request.getfixturevalue(name)
+    eye, rot = orbit_camera(*cfg.camera)
+    eye2, rot2 = orbit_camera(30.0, 15.0, 4.0)
+    w, h = 960, 540
+    frames = [(eye, rot, f) for f in range(24)] + [(eye2, rot2, f) for f in range(20)]
+
+    def run(flags):
+        out = []
+        with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=flags, tile_rank=tile[0],
+                      tile_world=tile[1]) as r:
+            r.upload_scene(tris, nodes)
+            r.upload_env(hdr)
+            for k, (e, m, f) in enumerate(frames):
+                r.render_frame(e, m, f, sync=False)
+                if k in (10, 20, 30):
+                    out.append(r.accum())
+            out.append(r.accum())
+            return out, r.stats()
+
+    a, sa = run(0)
+    b, sb = run(FLAG_SERIAL_FRAMES)
+    assert sa.frames_in_flight == 2 and sb.frames_in_flight == 1
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert sa.rays == sb.rays
