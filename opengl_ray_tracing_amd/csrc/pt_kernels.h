@@ -6,7 +6,10 @@
 
 namespace pt {
 
-constexpr int BLOCK = 256;        // 4 waves of 64
+#ifndef PT_BLOCK
+#define PT_BLOCK 256  // 64 and 128 measured: c2 +18 % / +8 %, c4 -6 % / -2 %
+#endif
+constexpr int BLOCK = PT_BLOCK;   // threads per block (256 = 4 waves of 64)
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 32
 #endif
@@ -54,9 +57,10 @@ static_assert((NUM_QUEUES & (NUM_QUEUES - 1)) == 0 && NUM_QUEUES <= 64, "NUM_QUE
 constexpr int RAY_SHARDS = 64;     // sharded ray counters (u64, one per 256-byte line)
 constexpr int RAY_SHARD_STRIDE = CTL_LINE_INTS / 2;  // in u64
 // control block layout (bytes)
-constexpr size_t CTL_QUEUES = 0;                                      // NUM_QUEUES padded int counters
-constexpr size_t CTL_STATS = 64 * 256;                                // 5 u64 cumulative fetch counters
-constexpr size_t CTL_RAYS = 65 * 256;                                 // RAY_SHARDS padded u64 counters
+constexpr int MAX_SLOTS = 4;  // frames in flight the control block has queue counters for (pt_runtime.cpp PIPE)
+constexpr size_t CTL_QUEUES = 0;  // MAX_SLOTS x NUM_QUEUES padded int counters
+constexpr size_t CTL_STATS = (size_t)MAX_SLOTS * 64 * 256;            // 5 u64 cumulative fetch counters
+constexpr size_t CTL_RAYS = CTL_STATS + 256;                          // RAY_SHARDS padded u64 counters
 constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
 #ifndef PT_FAST_TREE
 #define PT_FAST_TREE 1  // build and traverse the runtime's own tree (results checked against the reference's)

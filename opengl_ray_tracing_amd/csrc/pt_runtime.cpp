@@ -33,7 +33,10 @@ static constexpr int EV_RING = 64;
 // accumulation is updated in frame order and the image is bit for bit the one
 // of serial frames (c4: two overlapped frames measured 1.57x the throughput of
 // serial ones, tools/overlap_probe.py).
-static constexpr int PIPE = 2;
+#ifndef PT_PIPE
+#define PT_PIPE 2  // 1 (serial), 3 and 4 measured slower
+#endif
+static constexpr int PIPE = PT_PIPE;
 static_assert(PIPE * NUM_QUEUES * CTL_LINE_INTS * 4 <= (int)CTL_STATS, "queue counters of every slot fit the control block");
 
 #ifndef PT_TILE_GROUP
@@ -740,14 +743,14 @@ static int deviceHdrCache(pt_ctx* ctx, const float* hdr, int w, int h, float4* o
   float* scratch = nullptr;
   CK(hipMalloc(&d3, n * 3 * sizeof(float)));
   if (hipMalloc(&scratch, (2 * n + 2 * (size_t)w + 1) * sizeof(float)) != hipSuccess) {
-    hipFree(d3);
+    (void)hipFree(d3);
     return fail(ctx, PT_E_NOMEM, "hdr cache scratch");
   }
   hipError_t e = hipMemcpyAsync(d3, hdr, n * 3 * sizeof(float), hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess) e = launchHdrCache(d3, w, h, out, scratch, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  hipFree(d3);
-  hipFree(scratch);
+  (void)hipFree(d3);
+  (void)hipFree(scratch);
   if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("hdr cache: ") + hipGetErrorString(e));
   return PT_OK;
 }
@@ -815,7 +818,7 @@ int pt_hdr_cache_device(pt_ctx* ctx, const float* hdr, int w, int h, float* cach
   std::vector<float4> b(rc ? 0 : n);
   if (!rc && hipMemcpy(b.data(), d, n * sizeof(float4), hipMemcpyDeviceToHost) != hipSuccess)
     rc = fail(ctx, PT_E_HIP, "pt_hdr_cache_device: copy");
-  hipFree(d);
+  (void)hipFree(d);
   if (rc) return rc;
   for (size_t k = 0; k < n; k++) {
     cache_out[3 * k] = b[k].x;

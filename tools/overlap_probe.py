@@ -24,7 +24,11 @@ def main():
     ap.add_argument("--k", type=int, nargs="*", default=[1, 2, 3, 4])
     ap.add_argument("--tile-world", type=int, default=1)
     ap.add_argument("--frames", type=int, default=40)
+    ap.add_argument("--variant", default=None, help="an in-tree tuning build (tools/tune.py --build)")
     a = ap.parse_args()
+    if a.variant:
+        from opengl_ray_tracing_amd import _native
+        _native.use_variant(a.variant)
     from opengl_ray_tracing_amd import Renderer, orbit_camera, scenes
     cfg, tris, nodes, hdr = scenes.build_config(a.config)
     eye, rot = orbit_camera(*cfg.camera)
@@ -47,7 +51,7 @@ def main():
         dt = time.perf_counter() - t0
         ms_per_frame = 1e3 * dt / (a.frames * k)
         base = base or ms_per_frame
-        print(json.dumps({"config": a.config, "tile_world": a.tile_world, "k": k,
+        print(json.dumps({"variant": a.variant, "config": a.config, "tile_world": a.tile_world, "k": k,
                           "ms_per_frame": round(ms_per_frame, 4), "speedup": round(base / ms_per_frame, 3)}), flush=True)
         for r in rs:
             r.close()

@@ -27,10 +27,17 @@ def main():
     ap.add_argument("--ranks", default="all")
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--res", type=int, nargs=2, default=None, help="override the config's width height")
+    ap.add_argument("--variant", default=None, help="an in-tree tuning build (tools/tune.py --build)")
     a = ap.parse_args()
+    if a.variant:
+        from opengl_ray_tracing_amd import _native
+        _native.use_variant(a.variant)
     from opengl_ray_tracing_amd import Renderer, orbit_camera, scenes
     cfg, tris, nodes, hdr = scenes.build_config(a.config)
     eye, rot = orbit_camera(*cfg.camera)
+    if a.res:
+        cfg.width, cfg.height = a.res
     for w in a.worlds:
         ranks = range(w) if a.ranks == "all" else [0]
         res = []
@@ -53,7 +60,8 @@ def main():
                             "wall_ms": round(wall, 4), "rays": st.rays // st.launches,
                             "split_items": st.split_items, "runtime_tree": st.runtime_tree})
         worst = max(x["wall_ms"] for x in res)
-        print(json.dumps({"config": a.config, "world": w, "worst_wall_ms": worst, "ranks": res}), flush=True)
+        print(json.dumps({"variant": a.variant, "config": a.config, "res": [cfg.width, cfg.height], "flags": a.flags, "world": w,
+                          "worst_wall_ms": worst, "ranks": res}), flush=True)
 
 
 if __name__ == "__main__":
