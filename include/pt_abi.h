@@ -53,6 +53,7 @@ extern "C" {
 #define PT_FLAG_NO_TILE_ORDER 0x20u /* megakernel: hand out tiles in fixed order, not longest-first */
 #define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */
 #define PT_FLAG_SERIAL_FRAMES 0x80u /* megakernel: no frames in flight (each frame starts after the previous one ends) */
+#define PT_FLAG_NO_BINS 0x100u    /* megakernel: camera rays walk the BVH (no per-tile camera-ray bins) */
 
 /* in-process multi-GPU (pt_config.n_devices > 1) */
 #define PT_MAX_DEVICES 8

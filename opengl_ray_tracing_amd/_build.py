@@ -48,6 +48,7 @@ SOURCES = {
     "pt_regen.o": ("hip", CSRC / "pt_regen.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h", CSRC / "pt_trace.h",
                                                    INCLUDE / "pt_fmath.h"]),
     "pt_envcache.o": ("hip", CSRC / "pt_envcache.hip", [CSRC / "pt_kernels.h"]),
+    "pt_primary.o": ("hip", CSRC / "pt_primary.hip", [CSRC / "pt_kernels.h"]),
     "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", CSRC / "pt_wavefront.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
                                                        INCLUDE / "pt_fmath.h", CSRC / "pt_rccl.h"]),
     "pt_rccl.o": ("cxx", CSRC / "pt_rccl.cpp", [CSRC / "pt_rccl.h"]),

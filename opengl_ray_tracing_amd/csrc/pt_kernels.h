@@ -134,6 +134,11 @@ struct RenderParams {
   // sample colour here (float4, w unused) and leave the running mean to mixKernel, which
   // runs in frame order; null = mix into accum in place (IS:868-871)
   float4* col;
+  // camera-ray bins (pt_primary.hip): per 8x8 tile of the whole image, binStart[t] ..
+  // binStart[t+1] index binTris; null = every camera ray walks the BVH
+  const int* binStart;
+  const int* binTris;
+  int binTilesX, binTilesY;
   int* queue;           // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
   int perQueue;         // items per queue
   int numItems;         // 8x8 wave tiles owned by this rank
@@ -179,6 +184,29 @@ struct PackParams {
   int width, height, shardSize, shardsX, rank, world;
   long count;
 };
+
+// camera-ray bins of one camera (pt_primary.hip), device buffers owned by the context
+#ifndef PT_BIN_CAP
+#define PT_BIN_CAP 32  // a tile whose bin holds more triangles traces its camera rays through the BVH
+#endif
+#ifndef PT_BINS
+#define PT_BINS 1      // 0: no camera-ray bins
+#endif
+struct PrimaryBins {
+  int4* rect = nullptr;      // per triangle: its tile rectangle
+  int* triCount = nullptr;   // per triangle: its tiles (+1: the scan total)
+  int* triOffset = nullptr;
+  int* tileCount = nullptr;  // per tile: its triangles, then the fill cursors
+  int* binStart = nullptr;   // per tile (+1)
+  int* binTris = nullptr;
+  void* tmp = nullptr;       // hipcub scan scratch
+  size_t rectCap = 0, triCountCap = 0, triOffsetCap = 0, tileCountCap = 0, binStartCap = 0, binTrisCap = 0,
+         tmpBytes = 0;
+  int tilesX = 0, tilesY = 0, entries = 0;
+};
+hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, int height, const float4* geo, int nTri,
+                            PrimaryBins& b, hipStream_t s);
+void freePrimaryBins(PrimaryBins& b);
 
 // calculateHdrCache on the device (pt_envcache.hip); scratch: 2*w*h + 2*w + 1 floats
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);

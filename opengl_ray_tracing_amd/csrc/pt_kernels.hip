@@ -258,7 +258,49 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
   bool tie;
   int tri;
-  if (p.scene.fast) {  // through the runtime's tree, checked against the reference's
+  // camera-ray bins (pt_primary.hip): the tile's candidate triangles, each tested
+  // with hitTriangle's exact arithmetic (IS:251-301); the closest stands when no
+  // other candidate ties it and the reference traversal reaches it (refReachable),
+  // else the ray is retraced in the reference order
+  int b0 = 0, b1 = 0;  // an 8x8 tile of a shard wholly outside the image (no valid lane) has no bin
+  if (p.binStart) {
+    // every lane calls this function, so the first active lane is lane 0, whose pixel lies in the tile
+    const int tx = __builtin_amdgcn_readfirstlane(px) >> 3, ty = __builtin_amdgcn_readfirstlane(py) >> 3;
+    if (tx < p.binTilesX && ty < p.binTilesY) {
+      const int tile = ty * p.binTilesX + tx;
+      b0 = p.binStart[tile];
+      b1 = p.binStart[tile + 1];
+    }
+  }
+  if (p.binStart && b1 - b0 <= PT_BIN_CAP) {
+    float tbest = PT_INF;
+    int best = -1;
+    tie = false;
+    for (int k = b0; k < b1; k++) {
+      const int i = p.binTris[k];
+      const float4* g = p.scene.geo + 4 * (size_t)i;
+      float tt;
+      const bool h = valid && triTest(g[0], g[1], g[2], g[3], eye, dir, PT_INF, tt);
+      if (h && tt == tbest) tie = true;
+      if (h && tt < tbest) {
+        tbest = tt;
+        best = i;
+      }
+    }
+    if (valid) C.rays++;
+    tri = best;
+    t = tbest;
+    if (valid && (tie || (tri >= 0 && !refReachable(p.scene, tri, eye, dir, t)))) {
+      C.rays--;  // the same ray, counted once
+      tri = traceRay<false, CULL, false, Stack>(p.scene, eye, dir, t, st, C);
+    }
+  } else if (!p.packets) {  // a tree too deep for the packet stack: each ray on its own
+    tri = -1;
+    if (valid) {
+      Tracer<CULL, false> tr{p.scene, st, C, top};
+      tri = tr.trace(eye, dir, t);
+    }
+  } else if (p.scene.fast) {  // through the runtime's tree, checked against the reference's
     const int pos = tracePacket<CULL, FAST_KIND>(fastView(p.scene), eye, dir, valid, t, tie, pstack, C, top);
     tri = pos >= 0 ? p.scene.fastTri[pos] : -1;
     if (valid && (tie || (tri >= 0 && !refReachable(p.scene, tri, eye, dir, t)))) {
@@ -644,7 +686,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     const int px = gx * p.shardSize + (s % sub) * 8 + (k & 7);
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
     const bool valid = lane < nLanes && px < p.width && py < p.height;
-    if (!COUNT && p.packets) {
+    if (!COUNT && (p.packets || p.binStart)) {
       float t;
       const int tri = primaryPacket<CULL>(p, px, py, valid, st, C, top, pstack, t);
       if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);

@@ -101,6 +101,11 @@ struct pt_ctx {
   // tree / tile-split policy probe (probePolicy): frames since the probe (re)started,
   // the summed frame times of each policy, the decision
   int probeFrame = 0;
+  // camera-ray bins (pt_primary.hip) of the camera and scene they were built for
+  PrimaryBins bins;
+  bool binsValid = false;
+  float binEye[3] = {}, binCam[16] = {};
+  unsigned sceneVersion = 0, binVersion = 0;
   // frames in flight (PIPE slots; see PIPE above)
   bool pipe = false;                        // this context pipelines its megakernel frames
   hipStream_t slotStream[PIPE] = {};
@@ -347,6 +352,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
+  freePrimaryBins(ctx->bins);
   for (int k = 0; k < PIPE; k++) {
     if (ctx->slotStream[k]) (void)hipStreamSynchronize(ctx->slotStream[k]);
     dfree(ctx->d_col[k]);
@@ -704,6 +710,7 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
       (rc = upload(ctx, &ctx->d_refParent, h.parent)) || (rc = upload(ctx, &ctx->d_refBox, h.refBox)) ||
       (rc = upload(ctx, &ctx->d_leafBox, h.leafBox)))
     return rc;
+  ctx->sceneVersion++;  // camera-ray bins are rebuilt for the new triangles
   ctx->fRoot = h.fastTree.rootRef;
   ctx->fnDev = h.fastTree.nDev;
   ctx->fDepth = h.fastTree.depth;
@@ -1248,6 +1255,26 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
+  // camera-ray bins, rebuilt when the camera or the scene changed (the previous frame
+  // has ended first: it may still read the old bins); they need the reference facts
+  // refReachable checks a bin's winner against
+  const bool bins = PT_BINS && !regen && !count && ctx->fastReady && !(c.flags & PT_FLAG_NO_BINS);
+  if (bins) {
+    if (!ctx->binsValid || ctx->binVersion != ctx->sceneVersion || std::memcmp(ctx->binEye, eye, sizeof(ctx->binEye)) ||
+        std::memcmp(ctx->binCam, cameraRotate, sizeof(ctx->binCam))) {
+      if (ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
+      ctx->binsValid = false;
+      CK(buildPrimaryBins(eye, cameraRotate, c.width, c.height, ctx->d_geo, ctx->nTri, ctx->bins, S));
+      std::memcpy(ctx->binEye, eye, sizeof(ctx->binEye));
+      std::memcpy(ctx->binCam, cameraRotate, sizeof(ctx->binCam));
+      ctx->binVersion = ctx->sceneVersion;
+      ctx->binsValid = true;
+    }
+    p.binStart = ctx->bins.binStart;
+    p.binTris = ctx->bins.binTris;
+    p.binTilesX = ctx->bins.tilesX;
+    p.binTilesY = ctx->bins.tilesY;
+  }
   p.tileOrder = ordered && ctx->orderValid[slot] ? order : nullptr;
   p.orderCap = orderCap;
   p.tileCost = cost;

@@ -33,6 +33,7 @@ FLAG_REGEN = 0x10
 FLAG_NO_TILE_ORDER = 0x20
 FLAG_REFERENCE_TREE = 0x40
 FLAG_SERIAL_FRAMES = 0x80
+FLAG_NO_BINS = 0x100
 GATHER = {"auto": 0, "copy": 1, "rccl": 2}
 
 

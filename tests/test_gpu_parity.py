@@ -266,3 +266,33 @@ def test_pipelined_frames_equal_serial_frames(request, name, tile):
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert sa.rays == sb.rays
+
+
+@pytest.mark.parametrize("name,integrator,tile", [("c2", "lambert", (0, 1)), ("c3", "mis", (0, 1)),
+                                                  ("c4", "mis", (0, 1)), ("c2", "lambert", (2, 3))])
+def test_camera_bins_equal_bvh_camera_rays(request, name, integrator, tile):
+    """Camera rays found through the per-tile camera-ray bins (the default; pt_primary.hip)
+    give the images of camera rays that walk the BVH (PT_FLAG_NO_BINS) bit for bit, with
+    the same rays -- across a camera move (the bins are rebuilt) and on a screen-tile shard."""
+    from opengl_ray_tracing_amd import FLAG_NO_BINS
+    cfg, tris, nodes, hdr = request.getfixturevalue(name)
+    cams = [orbit_camera(*cfg.camera), orbit_camera(40.0, 25.0, 3.0), orbit_camera(-70.0, -10.0, 6.0)]
+    w, h = 960, 540
+
+    def run(flags):
+        out = []
+        with Renderer(w, h, integrator, max_bounce=cfg.max_bounce, flags=flags, tile_rank=tile[0],
+                      tile_world=tile[1]) as r:
+            r.upload_scene(tris, nodes)
+            r.upload_env(hdr)
+            for e, m in cams:
+                for f in range(3):
+                    r.render_frame(e, m, f, sync=False)
+                out.append(r.accum())
+            return out, r.stats()
+
+    a, sa = run(0)
+    b, sb = run(FLAG_NO_BINS)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert sa.rays == sb.rays
