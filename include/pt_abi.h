@@ -26,7 +26,8 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats */
+#define PT_ABI_VERSION 3  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
+                             3: scene-upload fields at the end of pt_frame_stats, pt_build_bvh_device */
 
 /* error codes */
 #define PT_OK 0
@@ -54,6 +55,8 @@ extern "C" {
 #define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */
 #define PT_FLAG_SERIAL_FRAMES 0x80u /* megakernel: no frames in flight (each frame starts after the previous one ends) */
 #define PT_FLAG_NO_BINS 0x100u    /* megakernel: camera rays walk the BVH (no per-tile camera-ray bins) */
+#define PT_FLAG_HOST_ACCEL 0x200u /* pt_upload_scene builds the runtime's own tree on the host (threaded binned
+                                     SAH) instead of on the GPU (pt_build.hip) */
 
 /* in-process multi-GPU (pt_config.n_devices > 1) */
 #define PT_MAX_DEVICES 8
@@ -108,6 +111,12 @@ typedef struct pt_frame_stats {
   int gather;           /* PT_GATHER_COPY / PT_GATHER_RCCL in use (0 with one device) */
   int frames_in_flight; /* megakernel frames that may overlap (1 = serial; >1: kernel_ms of
                            overlapping launches add up to more than the wall time) */
+  /* the last pt_upload_scene (kept across pt_reset_stats) */
+  float upload_ms;      /* its wall time: host re-layout, copies and the runtime tree build */
+  float accel_build_ms; /* wall time of the runtime tree's build (GPU, or host with PT_FLAG_HOST_ACCEL) */
+  int accel_device;     /* 1: the runtime tree was built on the GPU, 0: on the host, -1: none */
+  int accel_nodes;      /* the runtime tree's nodes (internal + leaves) */
+  int accel_depth;      /* and its depth (root = 1) */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;
@@ -152,6 +161,17 @@ int pt_render_frame(pt_ctx* ctx, const float eye[3], const float cameraRotate[16
 /* Same without synchronising or downloading. */
 int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16],
                           uint32_t frameCounter);
+
+/* The GPU binned-SAH builder (pt_build.hip), exposed as a scene
+ * builder in the reference's node encoding -- the role of buildBVH / buildBVHwithSAH
+ * (OpenglRayTracing/main.cpp:376-551), with pt_scene.h PT_BVH_BINNED_SAH's split rule.
+ * tris = nTriangles x 36 f32 (Triangle_encoded; only p1..p3 are read). Writes
+ * *nNodes_out nodes (12 f32 each: dummy node 0, root 1, leaves of <= leafSize
+ * triangles whose ranges index the built order) to nodes_out when they fit in
+ * max_nodes (else PT_E_INVALID, *nNodes_out still set), and order_out[i] = the input
+ * index of the triangle at built position i (nTriangles ints). */
+int pt_build_bvh_device(pt_ctx* ctx, const float* tris, int nTriangles, int leafSize, float* nodes_out,
+                        int max_nodes, int* nNodes_out, int* order_out);
 
 /* Batch hitBVH (pass1.fsh:335-382; BVH/main.cpp:571 debug-ray query). rays =
  * n x 6 f32 (origin, direction); miss -> t = 2147483648.f, tri = -1. */

@@ -49,6 +49,7 @@ SOURCES = {
                                                    INCLUDE / "pt_fmath.h"]),
     "pt_envcache.o": ("hip", CSRC / "pt_envcache.hip", [CSRC / "pt_kernels.h"]),
     "pt_primary.o": ("hip", CSRC / "pt_primary.hip", [CSRC / "pt_kernels.h"]),
+    "pt_build.o": ("hip", CSRC / "pt_build.hip", [CSRC / "pt_kernels.h"]),
     "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", CSRC / "pt_wavefront.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
                                                        INCLUDE / "pt_fmath.h", CSRC / "pt_rccl.h"]),
     "pt_rccl.o": ("cxx", CSRC / "pt_rccl.cpp", [CSRC / "pt_rccl.h"]),

@@ -13,7 +13,7 @@ from . import _build
 
 _lib = None
 
-ABI_VERSION = 2  # include/pt_abi.h PT_ABI_VERSION
+ABI_VERSION = 3  # include/pt_abi.h PT_ABI_VERSION
 c_float_p = C.POINTER(C.c_float)
 c_int_p = C.POINTER(C.c_int)
 
@@ -35,6 +35,8 @@ class PtFrameStats(C.Structure):
         ("kernel_ms_total", C.c_float), ("launches", C.c_int), ("max_stack", C.c_int),
         ("split_items", C.c_int), ("runtime_tree", C.c_int),
         ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int), ("frames_in_flight", C.c_int),
+        ("upload_ms", C.c_float), ("accel_build_ms", C.c_float), ("accel_device", C.c_int),
+        ("accel_nodes", C.c_int), ("accel_depth", C.c_int),
     ]
 
 
@@ -62,6 +64,7 @@ SIGNATURES = {
     "pt_render_frame": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32, c_float_p]),
     "pt_render_frame_async": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32]),
     "pt_trace_closest": (C.c_int, [C.c_void_p, c_float_p, C.c_int, c_float_p, c_int_p]),
+    "pt_build_bvh_device": (C.c_int, [C.c_void_p, c_float_p, C.c_int, C.c_int, c_float_p, C.c_int, c_int_p, c_int_p]),
     "pt_download_accum": (C.c_int, [C.c_void_p, c_float_p]),
     "pt_upload_accum": (C.c_int, [C.c_void_p, c_float_p]),
     "pt_clear_accum": (C.c_int, [C.c_void_p]),

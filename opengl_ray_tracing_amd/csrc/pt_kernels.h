@@ -208,6 +208,29 @@ hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, 
                             PrimaryBins& b, hipStream_t s);
 void freePrimaryBins(PrimaryBins& b);
 
+// The runtime's own tree built on the device (pt_build.hip): a binned-SAH tree
+// over the triangles of geo (SceneView::geo layout), its wide records with
+// every box widened by inflate of its own magnitude plus inflateRelAbs x the
+// scene's largest coordinate (pt_runtime.cpp encodeWideTree), the pair records
+// in its leaf order and that order. Device buffers owned by the caller
+// (freeAccelBuild); the stream is synchronised on return.
+struct BuildNode {  // 64 B, breadth-first ids (root 0)
+  float4 lo;        // triangle box lo; w: first position (int bits)
+  float4 hi;        // triangle box hi; w: triangle count (int bits)
+  float4 clo;       // centroid bounds lo; w: left child id (int bits, -1 = leaf)
+  float4 chi;       // centroid bounds hi; w: right child id
+};
+struct AccelBuild {
+  float4* bvh = nullptr;    // nDev wide records (4 float4 each)
+  float4* pairs = nullptr;  // nTri pair records (PAIR_F4 float4 each), leaf order
+  int* order = nullptr;     // position -> uploaded triangle index
+  BuildNode* nodes = nullptr;  // the nNodes build nodes (leaves: count <= leafSize)
+  int rootRef = REF_NONE, nDev = 0, depth = 0, nNodes = 0;
+};
+hipError_t buildAccelDevice(const float4* geo, int nTri, int leafSize, float inflate, float inflateRelAbs,
+                            AccelBuild& out, hipStream_t s);
+void freeAccelBuild(AccelBuild& a);
+
 // calculateHdrCache on the device (pt_envcache.hip); scratch: 2*w*h + 2*w + 1 floats
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);
 // hdr[k].w = cache[k].z, samp[k] = cache[k].xy (the Env render layout)

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -79,6 +80,9 @@ struct pt_ctx {
   float4* d_refBox = nullptr;
   float4* d_leafBox = nullptr;
   int fRoot = REF_NONE, fnDev = 0, fDepth = 0;
+  // the last pt_upload_scene (pt_frame_stats upload_ms, accel_*)
+  float uploadMs = 0.0f, accelMs = 0.0f;
+  int accelDevice = -1, accelNodes = 0, accelDepth = 0;
   int rootRef = REF_NONE;
   int nTri = 0, nNodes = 0, depth = 0, maxStack = 0;
   // env
@@ -582,6 +586,9 @@ struct SceneHost {
   WideTree ref;
   // the runtime's own tree and the reference facts its results are checked against
   bool fast = false;
+  bool deviceBuild = false;  // the tree itself is built on each device (pt_build.hip) by uploadScene
+  float accelMs = 0.0f;      // host build time (deviceBuild false)
+  int accelNodes = 0;
   WideTree fastTree;
   std::vector<float4> fpairs, refBox, leafBox;
   std::vector<int> order, leafOf, parent;
@@ -592,7 +599,7 @@ struct SceneHost {
 // (pt_trace.h refReachable): each triangle's reference leaf and its box, every
 // reference node's parent and box. Any triangle in two reference leaves, or a
 // failed build, leaves the runtime on the reference tree alone (h.fast false).
-static void prepareAccel(const float* tris, int nTri, const float* nodes, int nNodes, SceneHost& h) {
+static void prepareAccel(const float* tris, int nTri, const float* nodes, int nNodes, SceneHost& h, bool hostBuild) {
   h.fast = false;
   if (!PT_FAST_TREE) return;
   auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
@@ -645,8 +652,17 @@ static void prepareAccel(const float* tris, int nTri, const float* nodes, int nN
       h.leafBox[2 * (size_t)i + 1] = h.refBox[2 * (size_t)leafOf[i] + 1];
     }
   }
+  // the tree itself: on the GPU by uploadScene (pt_build.hip), or here (scene.cpp's threaded
+  // binned SAH; the quantized record kind is encoded on the host only)
+  if (!hostBuild && !FAST_QUANT) {
+    h.deviceBuild = true;
+    h.fast = true;
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
   std::vector<float> an;
   if (pt::buildAccel(tris, nTri, PT_ACCEL_LEAF, an, h.order) < 0 || an.size() / 12 >= (1u << 24)) return;
+  h.accelNodes = (int)(an.size() / 12) - 1;
 
   // widened by 1e-5 of each box's own magnitude plus 3e-5 of the scene's: above
   // the rounding of a slab test (~1.2e-7 x the origin-box distance) for ray origins
@@ -659,11 +675,13 @@ static void prepareAccel(const float* tris, int nTri, const float* nodes, int nN
            .empty())
     return;
   buildPairs(h.geo, h.order.data(), nTri, h.fpairs);
+  h.accelMs = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h.fast = true;
 }
 
 // host-side re-layout of the caller's arrays (pt_upload_scene); "" or the reason they are malformed
-static std::string prepareScene(const float* tris, int nTri, const float* nodes, int nNodes, SceneHost& h) {
+static std::string prepareScene(const float* tris, int nTri, const float* nodes, int nNodes, SceneHost& h,
+                                bool hostBuild) {
   h.nTri = nTri;
   h.nNodes = nNodes;
   // geometry records (+1 zero record past the last triangle)
@@ -681,7 +699,7 @@ static std::string prepareScene(const float* tris, int nTri, const float* nodes,
   std::string bad = encodeWideTree(nodes, nNodes, nTri, 0.0f, h.ref);
   if (!bad.empty()) return bad;
   buildPairs(h.geo, nullptr, nTri, h.pairs);
-  prepareAccel(tris, nTri, nodes, nNodes, h);
+  prepareAccel(tris, nTri, nodes, nNodes, h, hostBuild);
   return "";
 }
 
@@ -704,17 +722,50 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   ctx->depth = h.ref.depth;
   ctx->maxStack = h.ref.depth + 1;
   ctx->fastReady = false;
+  ctx->accelDevice = -1;
+  ctx->accelMs = 0.0f;
+  ctx->accelNodes = ctx->accelDepth = 0;
   if (!h.fast) return PT_OK;
-  if ((rc = upload(ctx, &ctx->d_fbvh, h.fastTree.bvh)) || (rc = upload(ctx, &ctx->d_fpairs, h.fpairs)) ||
-      (rc = upload(ctx, &ctx->d_fastTri, h.order)) || (rc = upload(ctx, &ctx->d_refLeafOf, h.leafOf)) ||
-      (rc = upload(ctx, &ctx->d_refParent, h.parent)) || (rc = upload(ctx, &ctx->d_refBox, h.refBox)) ||
-      (rc = upload(ctx, &ctx->d_leafBox, h.leafBox)))
+  if ((rc = upload(ctx, &ctx->d_refLeafOf, h.leafOf)) || (rc = upload(ctx, &ctx->d_refParent, h.parent)) ||
+      (rc = upload(ctx, &ctx->d_refBox, h.refBox)) || (rc = upload(ctx, &ctx->d_leafBox, h.leafBox)))
     return rc;
+  if (h.deviceBuild) {
+    // the runtime's tree built here, from the geometry records just uploaded (pt_build.hip)
+    const auto t0 = std::chrono::steady_clock::now();
+    AccelBuild ab;
+    hipError_t e = buildAccelDevice(ctx->d_geo, h.nTri, PT_ACCEL_LEAF, 1e-5f, 3e-5f, ab, ctx->stream);
+    if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("device tree build: ") + hipGetErrorString(e));
+    dfree(ab.nodes);
+    if (ab.nNodes + 1 >= (1 << 24)) {  // as the host path: no runtime tree of 2^24 nodes or more
+      freeAccelBuild(ab);
+      return PT_OK;
+    }
+    dfree(ctx->d_fbvh);
+    dfree(ctx->d_fpairs);
+    dfree(ctx->d_fastTri);
+    ctx->d_fbvh = ab.bvh;
+    ctx->d_fpairs = ab.pairs;
+    ctx->d_fastTri = ab.order;
+    ctx->fRoot = ab.rootRef;
+    ctx->fnDev = ab.nDev;
+    ctx->fDepth = ab.depth;
+    ctx->accelMs = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->accelDevice = 1;
+    ctx->accelNodes = ab.nNodes;
+  } else {
+    if ((rc = upload(ctx, &ctx->d_fbvh, h.fastTree.bvh)) || (rc = upload(ctx, &ctx->d_fpairs, h.fpairs)) ||
+        (rc = upload(ctx, &ctx->d_fastTri, h.order)))
+      return rc;
+    ctx->fRoot = h.fastTree.rootRef;
+    ctx->fnDev = h.fastTree.nDev;
+    ctx->fDepth = h.fastTree.depth;
+    ctx->accelMs = h.accelMs;
+    ctx->accelDevice = 0;
+    ctx->accelNodes = h.accelNodes;
+  }
+  ctx->accelDepth = ctx->fDepth;
   ctx->sceneVersion++;  // camera-ray bins are rebuilt for the new triangles
-  ctx->fRoot = h.fastTree.rootRef;
-  ctx->fnDev = h.fastTree.nDev;
-  ctx->fDepth = h.fastTree.depth;
-  ctx->maxStack = std::max(ctx->maxStack, h.fastTree.depth + 1);
+  ctx->maxStack = std::max(ctx->maxStack, ctx->fDepth + 1);
   ctx->fastReady = true;
   return PT_OK;
 }
@@ -735,11 +786,62 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTri, const float* nodes
   if (!ctx || !tris || !nodes) return PT_E_INVALID;
   if (nTri < 1 || nNodes < 2) return fail(ctx, PT_E_BADSCENE, "need >= 1 triangle and >= 2 nodes (dummy 0, root 1)");
   if (nTri > MAX_TRIS) return fail(ctx, PT_E_BADSCENE, "too many triangles for the leaf encoding");
+  const auto t0 = std::chrono::steady_clock::now();
   SceneHost h;
-  std::string bad = prepareScene(tris, nTri, nodes, nNodes, h);
+  std::string bad = prepareScene(tris, nTri, nodes, nNodes, h, (ctx->cfg.flags & PT_FLAG_HOST_ACCEL) != 0);
   if (!bad.empty()) return fail(ctx, PT_E_BADSCENE, bad);
   for (pt_ctx* m : members(ctx))
     if (int rc = uploadScene(m, tris, h)) return fromPeer(ctx, m, rc);
+  ctx->uploadMs = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return PT_OK;
+}
+
+int pt_build_bvh_device(pt_ctx* ctx, const float* tris, int nTri, int leafSize, float* nodes_out, int maxNodes,
+                        int* nNodesOut, int* orderOut) {
+  if (!ctx || !tris || !nodes_out || !nNodesOut || !orderOut || nTri < 1 || leafSize < 1 || leafSize > MAX_LEAF)
+    return PT_E_INVALID;
+  if (nTri > MAX_TRIS) return fail(ctx, PT_E_BADSCENE, "too many triangles for the leaf encoding");
+  if (int rc = syncStreams(ctx)) return rc;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  // the builder reads p1..p3 of the geometry records (the normal and plane offset only feed the pair records)
+  std::vector<float4> geo((size_t)nTri * 4, make_float4(0, 0, 0, 0));
+  for (int i = 0; i < nTri; i++)
+    for (int k = 0; k < 3; k++) {
+      const float* v = tris + (size_t)i * 36 + 3 * k;
+      geo[4 * (size_t)i + k] = make_float4(v[0], v[1], v[2], 0.0f);
+    }
+  float4* dgeo = nullptr;
+  if (int rc = upload(ctx, &dgeo, geo)) return rc;
+  AccelBuild ab;
+  hipError_t e = buildAccelDevice(dgeo, nTri, leafSize, 0.0f, 0.0f, ab, ctx->stream);
+  dfree(dgeo);
+  if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("device tree build: ") + hipGetErrorString(e));
+  const int M = ab.nNodes;
+  *nNodesOut = M + 1;
+  std::vector<BuildNode> bn(M);
+  e = hipMemcpy(bn.data(), ab.nodes, (size_t)M * sizeof(BuildNode), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(orderOut, ab.order, (size_t)nTri * sizeof(int), hipMemcpyDeviceToHost);
+  freeAccelBuild(ab);
+  if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("device tree download: ") + hipGetErrorString(e));
+  if (M + 1 > maxNodes) return fail(ctx, PT_E_INVALID, "nodes_out holds fewer than *nNodes_out nodes");
+  // the reference encoding (BVHNode_encoded, main.cpp:69-73, 688-716): build node k is node k + 1
+  std::memset(nodes_out, 0, sizeof(float) * 12 * (size_t)(M + 1));
+  for (int k = 0; k < M; k++) {
+    const BuildNode& b = bn[k];
+    float* o = nodes_out + 12 * (size_t)(k + 1);
+    int start, count, left, right;
+    std::memcpy(&start, &b.lo.w, 4);
+    std::memcpy(&count, &b.hi.w, 4);
+    std::memcpy(&left, &b.clo.w, 4);
+    std::memcpy(&right, &b.chi.w, 4);
+    const bool leaf = count <= leafSize;
+    o[0] = leaf ? 0.0f : (float)(left + 1);
+    o[1] = leaf ? 0.0f : (float)(right + 1);
+    o[3] = leaf ? (float)count : 0.0f;
+    o[4] = leaf ? (float)start : 0.0f;
+    o[6] = b.lo.x; o[7] = b.lo.y; o[8] = b.lo.z;
+    o[9] = b.hi.x; o[10] = b.hi.y; o[11] = b.hi.z;
+  }
   return PT_OK;
 }
 
@@ -1601,6 +1703,11 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->devices = 1;
   st->gather = 0;
   st->frames_in_flight = ctx->pipe ? PIPE : 1;
+  st->upload_ms = ctx->uploadMs;
+  st->accel_build_ms = ctx->accelMs;
+  st->accel_device = ctx->accelDevice;
+  st->accel_nodes = ctx->accelNodes;
+  st->accel_depth = ctx->accelDepth;
   const int ls = ctx->pipe && ctx->frameNo > 0 ? (int)((ctx->frameNo - 1) % PIPE) : 0;  // the last frame's slot
   if (ctx->d_order && ctx->orderValid[ls]) {
     int counts[NUM_QUEUES];

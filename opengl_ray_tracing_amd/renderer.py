@@ -34,6 +34,7 @@ FLAG_NO_TILE_ORDER = 0x20
 FLAG_REFERENCE_TREE = 0x40
 FLAG_SERIAL_FRAMES = 0x80
 FLAG_NO_BINS = 0x100
+FLAG_HOST_ACCEL = 0x200
 GATHER = {"auto": 0, "copy": 1, "rccl": 2}
 
 
@@ -54,6 +55,11 @@ class FrameStats:
     devices: int = 1
     gather: int = 0
     frames_in_flight: int = 1
+    upload_ms: float = 0.0
+    accel_build_ms: float = 0.0
+    accel_device: int = -1
+    accel_nodes: int = 0
+    accel_depth: int = 0
 
 
 def _fp(a: np.ndarray):
@@ -162,6 +168,20 @@ class Renderer:
                  "pt_trace_closest")
         return t, tri
 
+    def build_bvh_device(self, tris: np.ndarray, leaf_size: int = 4):
+        """pt_build_bvh_device: the GPU binned-SAH tree over tris (n x 36 f32) in the reference's
+        node encoding. Returns (nodes (m x 12 f32, dummy node 0, root 1), order (n int32: input
+        index of the triangle at each built position))."""
+        t = np.ascontiguousarray(tris, np.float32).reshape(-1, 36)
+        n = t.shape[0]
+        cap = 2 * n + 2
+        nodes = np.zeros((cap, 12), np.float32)
+        order = np.empty(n, np.int32)
+        m = C.c_int()
+        self._ck(self._lib.pt_build_bvh_device(self._h, _fp(t), n, int(leaf_size), _fp(nodes), cap, C.byref(m),
+                                               order.ctypes.data_as(_native.c_int_p)), "pt_build_bvh_device")
+        return nodes[:m.value].copy(), order
+
     def accum(self) -> np.ndarray:
         out = np.empty((self.height, self.width, 4), np.float32)
         self._ck(self._lib.pt_download_accum(self._h, _fp(out)), "pt_download_accum")
@@ -213,7 +233,8 @@ class Renderer:
         self._ck(self._lib.pt_get_stats(self._h, C.byref(s)), "pt_get_stats")
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
                           s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
-                          s.waves_per_simd, s.devices, s.gather, s.frames_in_flight)
+                          s.waves_per_simd, s.devices, s.gather, s.frames_in_flight, s.upload_ms,
+                          s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")
