@@ -121,9 +121,8 @@ struct Material {  // IS:41-56
   float subsurface, metallic, specular, specularTint, roughness, anisotropic;
   float sheen, sheenTint, clearcoat, clearcoatGloss;
 };
-// getMaterial IS:207-232 from the 36-float Triangle_encoded record
-__device__ __forceinline__ Material loadMaterial(const float* rec) {
-  const float4* q = reinterpret_cast<const float4*>(rec + 16);  // floats 16..35 (records are 144 B, 16 B aligned)
+// getMaterial IS:207-232 from floats 16..35 of a Triangle_encoded record (5 float4)
+__device__ __forceinline__ Material loadMaterial(const float4* q) {
   float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
   // floats: 16 17 18 | 19 20 21 | 22 23 24 | 25 26 27 | 28 29 30 | 31 32 33 | 34 35
   // emissive = 18,19,20; baseColor = 21,22,23; param1 = 24..26; param2 = 27..29; param3 = 30..32; param4 = 33..35

@@ -2,8 +2,7 @@
 // main.cpp:555-652) on the GPU, bit-identical to the host restatement
 // (scene.cpp pt_hdr_cache): every floating-point sum runs in the reference's
 // order. Its one inherently sequential step, the float sum of all luminances
-// in scanline order, is a single dependent chain; one wave streams the values
-// through LDS and lane 0 adds them. The per-column sums and prefix sums are
+// in scanline order, is a single dependent chain (hdrSumKernel). The per-column sums and prefix sums are
 // one thread per column (serial over rows, as the reference), the row prefix
 // is one thread, and the sample table is one thread per texel (two
 // lower_bound searches).
@@ -22,16 +21,42 @@ __global__ void hdrLumKernel(const float* hdr, float* lum, int n) {
   lum[k] = (float)((0.2 * R + 0.7 * G) + 0.1 * B);
 }
 
-// lumSum += lum, k = 0 .. n-1 in order (main.cpp:561-570)
-__global__ __launch_bounds__(64) void hdrSumKernel(const float* lum, int n, float* out) {
-  __shared__ float buf[4096];
+// lumSum += lum, k = 0 .. n-1 in order (main.cpp:561-570). A float sum is not
+// associative, so only this one dependent chain gives the reference's bits: no
+// parallel reduction can. Wave 1 streams the next 4096 values into one LDS
+// buffer while lane 0 of wave 0 adds the current buffer's, four values per
+// LDS read.
+constexpr int SUM_CHUNK = 4096;
+__global__ __launch_bounds__(128) void hdrSumKernel(const float* lum, int n, float* out) {
+  __shared__ float4 buf[2][SUM_CHUNK / 4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int chunks = (n + SUM_CHUNK - 1) / SUM_CHUNK;
+  auto load = [&](int c) {
+    float* b = reinterpret_cast<float*>(buf[c & 1]);
+    const int base = c * SUM_CHUNK, m = min(SUM_CHUNK, n - base);
+    for (int i = lane; i < SUM_CHUNK; i += 64) b[i] = i < m ? lum[base + i] : 0.0f;
+  };
+  if (w == 1 && chunks > 0) load(0);
+  __syncthreads();
   float sum = 0.0f;
-  for (int base = 0; base < n; base += 4096) {
-    const int m = min(4096, n - base);
-    for (int i = threadIdx.x; i < m; i += 64) buf[i] = lum[base + i];
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int i = 0; i < m; i++) sum += buf[i];
+  for (int c = 0; c < chunks; c++) {
+    if (w == 1 && c + 1 < chunks) {
+      load(c + 1);
+    } else if (w == 0 && lane == 0) {
+      const int m = min(SUM_CHUNK, n - c * SUM_CHUNK);
+      const float4* b = buf[c & 1];
+      int i = 0;
+#pragma unroll 8
+      for (; i < m / 4; i++) {
+        const float4 v = b[i];
+        sum += v.x;
+        sum += v.y;
+        sum += v.z;
+        sum += v.w;
+      }
+      const float* t = reinterpret_cast<const float*>(b);
+      for (int k = 4 * i; k < m; k++) sum += t[k];
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) *out = sum;
@@ -120,7 +145,7 @@ hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* 
   float* lumSum = cdfX + w;
   const int B = 256;
   hipLaunchKernelGGL(hdrLumKernel, dim3((n + B - 1) / B), dim3(B), 0, s, hdr, pdf, n);
-  hipLaunchKernelGGL(hdrSumKernel, dim3(1), dim3(64), 0, s, pdf, n, lumSum);
+  hipLaunchKernelGGL(hdrSumKernel, dim3(1), dim3(128), 0, s, pdf, n, lumSum);
   hipLaunchKernelGGL(hdrPdfKernel, dim3((n + B - 1) / B), dim3(B), 0, s, pdf, n, lumSum);
   hipLaunchKernelGGL(hdrColumnKernel, dim3((w + 63) / 64), dim3(64), 0, s, pdf, w, h, margin, cdfY);
   hipLaunchKernelGGL(hdrRowPrefixKernel, dim3(1), dim3(1), 0, s, margin, w, cdfX);

@@ -80,6 +80,8 @@ constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
 #endif
 constexpr int PKT_DEPTH = 128;    // camera-ray packet stack entries per wave (LDS); deeper trees trace per ray
 constexpr int PAIR_F4 = 7;        // float4 per pair record (26 floats: p1, p2, p3, Ng, w of two triangles)
+constexpr int HIT_F4 = 4;         // float4 per hit record (SceneView::hitRec)
+constexpr int MAT_F4 = 5;         // float4 per material (SceneView::mats)
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;
 constexpr int MAX_LEAF = 1 << LEAF_CNT_BITS;
@@ -89,7 +91,13 @@ constexpr int MAX_TRIS = (1 << (31 - LEAF_CNT_BITS)) - 1;
 struct SceneView {
   const float4* geo;   // 4 float4 per triangle: (p1, w=dot(Ng,p1)), (p2, 0), (p3, 0), (Ng, 0)
   const float4* pairs; // PAIR_F4 float4 per triangle i: triangles i and i+1 component-interleaved (pt_trace.h pairTest)
-  const float* attr;   // 36 f32 per triangle: the Triangle_encoded record (normals, material)
+  // Shading data of a hit, read once per closest hit (finishHit): per triangle one
+  // 64-byte record {n1.xyz, n2.x}, {n2.yz, n3.xy}, {n3.z, material id, -, -} (the
+  // Triangle_encoded normals, floats 9..17), and the scene's distinct materials,
+  // MAT_F4 float4 each laid out as Triangle_encoded floats 16..35 (emissive at
+  // floats 18..20, IS:207-232). 64 + ~0 bytes per triangle instead of 144.
+  const float4* hitRec;
+  const float4* mats;
   const float4* bvh;   // 4 float4 per device node id (pt_runtime.cpp: top of the tree first, breadth-first)
   int nTop;            // device ids [0, nTop) are the top of the tree, staged in LDS by the megakernel
   int rootRef;         // encoded reference to node 1

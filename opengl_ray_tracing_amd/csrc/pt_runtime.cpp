@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -66,7 +68,9 @@ struct pt_ctx {
   // scene
   float4* d_geo = nullptr;
   float4* d_pairs = nullptr;  // triangles i and i+1 component-interleaved (SceneView::pairs)
-  float* d_attr = nullptr;
+  float4* d_hit = nullptr;   // per triangle: normals + material id (SceneView::hitRec)
+  float4* d_mats = nullptr;  // the distinct materials (SceneView::mats)
+  int nMats = 0;
   float4* d_bvh = nullptr;
   int nDevNodes = 0;  // internal nodes in d_bvh (device ids 0..nDevNodes-1)
   // the runtime's own tree (uploadAccel; SceneView::fast) and the reference
@@ -350,7 +354,7 @@ void pt_destroy(pt_ctx* ctx) {
   destroyGroup(ctx);
   (void)hipSetDevice(ctx->cfg.device_id);
   if (ctx->own) (void)hipStreamSynchronize(ctx->own);
-  dfree(ctx->d_geo); dfree(ctx->d_attr); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
+  dfree(ctx->d_geo); dfree(ctx->d_hit); dfree(ctx->d_mats); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
   dfree(ctx->d_fbvh); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri); dfree(ctx->d_refLeafOf);
   dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
@@ -583,6 +587,7 @@ static void buildPairs(const std::vector<float4>& geo, const int* order, int nTr
 struct SceneHost {
   int nTri = 0, nNodes = 0;
   std::vector<float4> geo, pairs;
+  std::vector<float4> hit, mats;  // SceneView::hitRec / mats
   WideTree ref;
   // the runtime's own tree and the reference facts its results are checked against
   bool fast = false;
@@ -696,6 +701,37 @@ static std::string prepareScene(const float* tris, int nTri, const float* nodes,
     h.geo[4 * i + 2] = make_float4(t[6], t[7], t[8], 0.0f);
     h.geo[4 * i + 3] = make_float4(N[0], N[1], N[2], 0.0f);
   }
+  // shading records: the normals and a material id per triangle; each distinct
+  // material (Triangle_encoded floats 18..35, compared bit for bit) stored once
+  h.hit.assign((size_t)nTri * HIT_F4, make_float4(0, 0, 0, 0));
+  {
+    std::map<std::array<uint32_t, 18>, int> ids;
+    std::array<uint32_t, 18> lastKey{};
+    int lastId = 0;
+    for (int i = 0; i < nTri; i++) {
+      const float* t = tris + (size_t)i * 36;
+      std::array<uint32_t, 18> key;
+      std::memcpy(key.data(), t + 18, sizeof(key));
+      int id;
+      if (i > 0 && key == lastKey) {  // meshes share one material: most lookups are this one
+        id = lastId;
+      } else if (auto it = ids.find(key); it == ids.end()) {
+        id = (int)ids.size();
+        ids.emplace(key, id);
+        for (int k = 0; k < MAT_F4; k++) h.mats.push_back(make_float4(t[16 + 4 * k], t[17 + 4 * k], t[18 + 4 * k], t[19 + 4 * k]));
+      } else {
+        id = it->second;
+      }
+      lastKey = key;
+      lastId = id;
+      float fid;
+      std::memcpy(&fid, &id, 4);
+      float4* r = &h.hit[(size_t)i * HIT_F4];
+      r[0] = make_float4(t[9], t[10], t[11], t[12]);
+      r[1] = make_float4(t[13], t[14], t[15], t[16]);
+      r[2] = make_float4(t[17], fid, 0.0f, 0.0f);
+    }
+  }
   std::string bad = encodeWideTree(nodes, nNodes, nTri, 0.0f, h.ref);
   if (!bad.empty()) return bad;
   buildPairs(h.geo, nullptr, nTri, h.pairs);
@@ -712,9 +748,8 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   if ((rc = upload(ctx, &ctx->d_pairs, h.pairs)) || (rc = upload(ctx, &ctx->d_geo, h.geo)) ||
       (rc = upload(ctx, &ctx->d_bvh, h.ref.bvh)))
     return rc;
-  dfree(ctx->d_attr);
-  CK(hipMalloc(&ctx->d_attr, (size_t)h.nTri * 36 * sizeof(float)));
-  CK(hipMemcpy(ctx->d_attr, tris, (size_t)h.nTri * 36 * sizeof(float), hipMemcpyHostToDevice));
+  if ((rc = upload(ctx, &ctx->d_hit, h.hit)) || (rc = upload(ctx, &ctx->d_mats, h.mats))) return rc;
+  ctx->nMats = (int)(h.mats.size() / MAT_F4);
   ctx->nTri = h.nTri;
   ctx->nNodes = h.nNodes;
   ctx->nDevNodes = h.ref.nDev;
@@ -1021,7 +1056,8 @@ static SceneView sceneView(const pt_ctx* ctx) {
   SceneView s;
   s.geo = ctx->d_geo;
   s.pairs = ctx->d_pairs;
-  s.attr = ctx->d_attr;
+  s.hitRec = ctx->d_hit;
+  s.mats = ctx->d_mats;
   s.bvh = ctx->d_bvh;
   s.nTop = std::min(LDS_NODES, ctx->nDevNodes);
   s.rootRef = ctx->rootRef;

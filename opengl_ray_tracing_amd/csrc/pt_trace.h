@@ -594,15 +594,14 @@ __device__ __forceinline__ void finishHit(const SceneView& S, int tri, V3 o, V3 
   float beta = (-(P.x - p3.x) * (p1.y - p3.y) + (P.y - p3.y) * (p1.x - p3.x)) /
                (-(p2.x - p3.x - 0.00005f) * (p1.y - p3.y + 0.00005f) + (p2.y - p3.y + 0.00005f) * (p1.x - p3.x + 0.00005f));
   float gama = 1.0f - alpha - beta;
-  const float* rec = S.attr + 36 * (size_t)tri;
-  const float4* q = reinterpret_cast<const float4*>(rec + 8);
-  float4 q0 = q[0], q1 = q[1], q2 = q[2];  // floats 8..19
-  V3 n1 = v3(q0.y, q0.z, q0.w), n2 = v3(q1.x, q1.y, q1.z), n3 = v3(q1.w, q2.x, q2.y);
+  const float4* q = S.hitRec + HIT_F4 * (size_t)tri;
+  const float4 q0 = q[0], q1 = q[1], q2 = q[2];  // Triangle_encoded floats 9..17 + the material id
+  V3 n1 = v3(q0.x, q0.y, q0.z), n2 = v3(q0.w, q1.x, q1.y), n3 = v3(q1.z, q1.w, q2.x);
   V3 Ns = normalize((n1 * alpha + n2 * beta) + n3 * gama);
   h.P = P;
   h.N = inside ? -Ns : Ns;
   h.viewDir = d;
-  h.m = loadMaterial(rec);
+  h.m = loadMaterial(S.mats + MAT_F4 * (size_t)__float_as_int(q2.y));
 }
 
 }  // namespace pt

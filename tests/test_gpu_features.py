@@ -239,11 +239,20 @@ def test_hdr_cache_on_gpu_equals_host(name):
     from pathlib import Path
 
     from opengl_ray_tracing_amd import calculate_hdr_cache, load_hdr
+    import time
     hdr = load_hdr(Path(__file__).parent / "golden" / name)
+    t0 = time.perf_counter()
     host = calculate_hdr_cache(hdr)
+    t1 = time.perf_counter()
     with Renderer(8, 8) as r:
+        r.hdr_cache_device(hdr)  # warm
+        t2 = time.perf_counter()
         dev = r.hdr_cache_device(hdr)
+        t3 = time.perf_counter()
     assert np.array_equal(dev.view(np.uint32), host.view(np.uint32))
+    # the one sequential float sum bounds the device path (pt_envcache.hip hdrSumKernel)
+    print(f"{name} {hdr.shape[1]}x{hdr.shape[0]}: host {1e3 * (t1 - t0):.1f} ms, device (incl. copies) "
+          f"{1e3 * (t3 - t2):.1f} ms")
 
 
 def test_launch_timing_ring_keeps_stats_exact():
