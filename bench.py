@@ -206,6 +206,7 @@ def main():
         roofline["time_basis"] = ("wall ms per frame (frames in flight)" if pipelined
                                   else "frame kernel HIP-event ms")
         roofline["launch_ms"] = round(kernel_ms_avg, 4)
+        roofline["kernel"] = ("regenKernel<%s>" if st.regen else "renderKernel<%s>") % cfg.integrator
         cpu = None
         if not args.no_cpu_baseline and n == 1:
             cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_seconds)
@@ -224,6 +225,7 @@ def main():
                        # the tree the timed frames traversed: the uploaded one, or the runtime's own
                        # binned-SAH tree with every result checked against the uploaded one
                        "traversal_tree": "runtime (checked against uploaded)" if st.runtime_tree else "uploaded",
+                       "frame_kernel": "path regeneration" if st.regen else "lock-step megakernel",
                        "waves_per_simd": st.waves_per_simd, "frames_in_flight": st.frames_in_flight,
                        "parallelism": (f"screen-tile x{n}" + (" + RCCL gather per frame" if n > 1 else ""))
                        if args.shard == "tiles" else

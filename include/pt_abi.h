@@ -55,6 +55,8 @@ extern "C" {
 #define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */
 #define PT_FLAG_SERIAL_FRAMES 0x80u /* megakernel: no frames in flight (each frame starts after the previous one ends) */
 #define PT_FLAG_NO_BINS 0x100u    /* megakernel: camera rays walk the BVH (no per-tile camera-ray bins) */
+#define PT_FLAG_MEGAKERNEL 0x400u /* large scenes (> 48 MB of records): the lock-step megakernel instead of
+                                     the path-regeneration kernel the Disney/MIS integrators default to there */
 #define PT_FLAG_HOST_ACCEL 0x200u /* pt_upload_scene builds the runtime's own tree on the host (threaded binned
                                      SAH) instead of on the GPU (pt_build.hip) */
 
@@ -117,6 +119,8 @@ typedef struct pt_frame_stats {
   int accel_device;     /* 1: the runtime tree was built on the GPU, 0: on the host, -1: none */
   int accel_nodes;      /* the runtime tree's nodes (internal + leaves) */
   int accel_depth;      /* and its depth (root = 1) */
+  int regen;            /* 1: the last frame ran the path-regeneration kernel (PT_FLAG_REGEN, or a large
+                           Disney/MIS scene), 0: the lock-step megakernel */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;

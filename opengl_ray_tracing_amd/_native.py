@@ -36,7 +36,7 @@ class PtFrameStats(C.Structure):
         ("split_items", C.c_int), ("runtime_tree", C.c_int),
         ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int), ("frames_in_flight", C.c_int),
         ("upload_ms", C.c_float), ("accel_build_ms", C.c_float), ("accel_device", C.c_int),
-        ("accel_nodes", C.c_int), ("accel_depth", C.c_int),
+        ("accel_nodes", C.c_int), ("accel_depth", C.c_int), ("regen", C.c_int),
     ]
 
 

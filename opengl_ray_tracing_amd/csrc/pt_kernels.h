@@ -24,9 +24,15 @@ constexpr int BLOCK = PT_BLOCK;   // threads per block (256 = 4 waves of 64)
 #define PT_COST_EMA 2  // order tiles by a running estimate of their cost, this frame's weighted 2^-PT_COST_EMA (0 = off)
 #endif
 #ifndef PT_WIDE_SCENE_MB
-#define PT_WIDE_SCENE_MB 64
+#define PT_WIDE_SCENE_MB 48  // 240 B of records per triangle (pairs, geometry, shading) + 64 per node: ~200k triangles
 #endif
 constexpr int WIDE_WAVES = 3;
+// ... and the Disney/MIS path-regeneration kernel (pt_regen.hip) compiled for 4 waves
+// per SIMD (128 VGPRs, 18 spilled) is their default frame kernel: with long paths
+// (c5: 16 bounces) a lane that takes a new pixel when its path ends beats the
+// lock-step megakernel, whose waves last as long as their longest path (c5: 10.0
+// -> 9.2 ms; on the L2-resident c4 the regen kernel is 3.6x slower)
+constexpr int WIDE_REGEN_WAVES = 4;
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
@@ -254,8 +260,9 @@ constexpr int REORDER_MAX = 4096;  // most groups per band the one-block LDS sor
 hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* ema, int* order, int perQueue, int orderCap,
                          int numItems, int group, int numWaves, int splitPct, hipStream_t s);
 hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, bool wide, int* nb);
-hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull);
-hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb);
+// the path-regeneration kernel (pt_regen.hip); wide: the large-scene variant (WIDE_REGEN_WAVES)
+hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool wide = false);
+hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb);
 int regenLdsStack();
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);

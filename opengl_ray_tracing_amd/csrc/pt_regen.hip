@@ -59,6 +59,10 @@ struct PathState {
 };
 
 __device__ __forceinline__ void writeAccum(const RenderParams& p, int px, int py, V3 color) {
+  if (p.col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in frame order
+    stStream(p.col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
+    return;
+  }
   float4* a = p.accum + (size_t)py * p.width + px;
   float4 old = ldStream(a);
   float w = 1.0f / (float)(p.frameCounter + 1u);
@@ -219,13 +223,24 @@ __device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int
   return false;
 }
 
-template <int INTEG, bool CULL>
-__global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U) void regenKernel(RenderParams p) {
+// WAVES > 0: compiled for that many waves per SIMD (large scenes, pt_runtime.cpp renderOne)
+template <int INTEG, bool CULL, int WAVES = 0>
+__global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U)) void regenKernel(
+    RenderParams p) {
   __shared__ int s_stack[REGEN_LDS_STACK * BLOCK];
   StackT<REGEN_LDS_STACK, BLOCK> st;
   st.lds = s_stack + threadIdx.x;
   st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * p.ovfDepth : nullptr;
   st.reset();
+  // the top of the uploaded tree (every ray's first node visits) staged in LDS once per block
+#if PT_LDS_NODES > 0
+  __shared__ float4 s_nodes[LDS_NODES * 4];
+  for (int i = threadIdx.x; i < p.scene.nTop * 4; i += BLOCK) s_nodes[i] = p.scene.bvh[i];
+  __syncthreads();
+  const float4* top = s_nodes;
+#else
+  const float4* top = nullptr;
+#endif
   Counters C = {0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -268,7 +283,8 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
     if (__ballot(active) == 0) break;
     if (!active) continue;
     float t;
-    const int tri = traceRay<false, CULL, false>(p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW);
+    const int tri = traceRay<false, CULL, false, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(
+        p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW, top);
     V3 color;
     if (!advance<INTEG>(p, s, tri, t, color)) {
       writeAccum(p, s.px, s.py, color);
@@ -279,27 +295,28 @@ __global__ __launch_bounds__(BLOCK, INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REG
 }
 
 template <int I>
-static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull) {
-  if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
+static const void* regenFn(bool cull, bool wide) {
+  if (wide && I != 0) return (const void*)regenKernel<I, true, WIDE_REGEN_WAVES>;
+  return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
+}
+template <int I>
+static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, bool wide) {
+  if (wide && cull && I != 0) hipLaunchKernelGGL((regenKernel<I, true, WIDE_REGEN_WAVES>), dim3(grid), dim3(BLOCK), 0, s, p);
+  else if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else hipLaunchKernelGGL((regenKernel<I, false>), dim3(grid), dim3(BLOCK), 0, s, p);
   return hipGetLastError();
 }
 
-hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull) {
+hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool wide) {
   switch (integrator) {
-    case 0: return launchRegenI<0>(p, grid, s, cull);
-    case 1: return launchRegenI<1>(p, grid, s, cull);
-    default: return launchRegenI<2>(p, grid, s, cull);
+    case 0: return launchRegenI<0>(p, grid, s, cull, wide);
+    case 1: return launchRegenI<1>(p, grid, s, cull, wide);
+    default: return launchRegenI<2>(p, grid, s, cull, wide);
   }
 }
 
-hipError_t regenBlocksPerCU(int integrator, bool cull, int* nb) {
-  const void* f;
-  switch (integrator) {
-    case 0: f = cull ? (const void*)regenKernel<0, true> : (const void*)regenKernel<0, false>; break;
-    case 1: f = cull ? (const void*)regenKernel<1, true> : (const void*)regenKernel<1, false>; break;
-    default: f = cull ? (const void*)regenKernel<2, true> : (const void*)regenKernel<2, false>; break;
-  }
+hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb) {
+  const void* f = integrator == 0 ? regenFn<0>(cull, wide) : integrator == 1 ? regenFn<1>(cull, wide) : regenFn<2>(cull, wide);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, f, BLOCK, 0);
 }
 

@@ -105,6 +105,7 @@ struct pt_ctx {
   int* d_cost = nullptr;   // per slot: per-tile cost of its last frame, longest item, split state, estimate
   int* d_order = nullptr;  // per slot: per-band work items for its next frame
   bool lastFast = false;    // the last megakernel frame traversed the runtime's tree
+  bool lastRegen = false;   // the last frame ran the path-regeneration kernel
   int lastWaves = 0;        // waves per SIMD of the last megakernel launch (occupancy query)
   // tree / tile-split policy probe (probePolicy): frames since the probe (re)started,
   // the summed frame times of each policy, the decision
@@ -1313,20 +1314,24 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     return renderWavefront(ctx, eye, cameraRotate, frameCounter, cull, stats, evb, eve);
   }
   // default: the lock-step persistent megakernel (also the fetch-counting
-  // variant); the path-regeneration kernel on request
-  const bool regen = !count && (c.flags & PT_FLAG_REGEN);
+  // variant); the path-regeneration kernel on request, and by default for the
+  // Disney/MIS integrators on large scenes (pt_kernels.h PT_WIDE_SCENE_MB,
+  // WIDE_REGEN_WAVES), whose walks are memory-latency bound and whose long paths
+  // leave a lock-step wave's lanes idle
+  const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + HIT_F4 * 16) + (size_t)ctx->nDevNodes * 64;
+  const bool wideScene = !count && cull && c.integrator != 0 && sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
+  const bool regen = !count && ((c.flags & PT_FLAG_REGEN) || (wideScene && !(c.flags & PT_FLAG_MEGAKERNEL)));
   // this frame's stream and per-frame buffers: slot frameNo % PIPE when pipelined
-  const bool piped = ctx->pipe && !regen && !count;
+  const bool piped = ctx->pipe && !count;
   const int slot = piped ? (int)(ctx->frameNo % PIPE) : 0;
   hipStream_t S = piped ? ctx->slotStream[slot] : ctx->stream;
   int nb = 0;
-  if (regen) CK(regenBlocksPerCU(c.integrator, cull, &nb));
-  // large scenes: the more-waves variant (pt_kernels.h PT_WIDE_SCENE_MB)
-  const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + 144) + (size_t)ctx->nDevNodes * 64;
-  const bool wide = !regen && !count && cull && c.integrator != 0 && sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
-  if (!regen) CK(renderBlocksPerCU(c.integrator, cull, count, wide, &nb));
+  const bool wide = wideScene;  // the more-waves variant of either kernel
+  if (regen) CK(regenBlocksPerCU(c.integrator, cull, wide, &nb));
+  else CK(renderBlocksPerCU(c.integrator, cull, count, wide, &nb));
   if (nb < 1) nb = 1;
-  ctx->lastWaves = regen ? 0 : nb * BLOCK / 64 / 4;  // 4 SIMDs per CU
+  ctx->lastWaves = nb * BLOCK / 64 / 4;  // 4 SIMDs per CU
+  ctx->lastRegen = regen;
   int grid = ctx->numCU * nb;
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, piped ? PIPE : 1);
@@ -1389,7 +1394,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // not to) and the split policy: probePolicy
   bool useFast = false;
   const int splitPct = probePolicy(ctx, frameCounter, ordered,
-                                   !count && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast);
+                                   !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast);
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
@@ -1436,7 +1441,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.waveTrace = dTrace;
 #endif
   CK(hipEventRecord(evb, S));
-  if (regen) CK(launchRegen(p, c.integrator, grid, S, cull));
+  if (regen) CK(launchRegen(p, c.integrator, grid, S, cull, wide));
   else CK(launchRender(p, c.integrator, grid, S, cull, count, wide));
 #if PT_WAVE_TRACE
   if (dTrace) {
@@ -1736,6 +1741,7 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->split_items = 0;
   st->runtime_tree = ctx->lastFast ? 1 : 0;
   st->waves_per_simd = ctx->lastWaves;
+  st->regen = ctx->lastRegen ? 1 : 0;
   st->devices = 1;
   st->gather = 0;
   st->frames_in_flight = ctx->pipe ? PIPE : 1;

@@ -35,6 +35,7 @@ FLAG_REFERENCE_TREE = 0x40
 FLAG_SERIAL_FRAMES = 0x80
 FLAG_NO_BINS = 0x100
 FLAG_HOST_ACCEL = 0x200
+FLAG_MEGAKERNEL = 0x400
 GATHER = {"auto": 0, "copy": 1, "rccl": 2}
 
 
@@ -60,6 +61,7 @@ class FrameStats:
     accel_device: int = -1
     accel_nodes: int = 0
     accel_depth: int = 0
+    regen: int = 0
 
 
 def _fp(a: np.ndarray):
@@ -234,7 +236,7 @@ class Renderer:
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
                           s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
                           s.waves_per_simd, s.devices, s.gather, s.frames_in_flight, s.upload_ms,
-                          s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth)
+                          s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth, s.regen)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

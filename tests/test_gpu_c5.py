@@ -15,7 +15,7 @@ import pytest
 
 import oracle
 import parity
-from opengl_ray_tracing_amd import FLAG_REFERENCE_TREE, Renderer, orbit_camera, scenes
+from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_REFERENCE_TREE, Renderer, orbit_camera, scenes
 
 pytestmark = pytest.mark.gpu
 
@@ -56,9 +56,11 @@ def test_c5_full_workload_binned_tree():
     assert tris.shape[0] > 1_000_000 and (cfg.width, cfg.height, cfg.max_bounce) == (3840, 2160, 16)
     g, st = render(cfg, tris, nodes, hdr)
     check_full_frame(cfg, g, st)
-    assert st.waves_per_simd == 3  # the large-scene variant (PT_WIDE_SCENE_MB)
-    b, sb = render(cfg, tris, nodes, hdr, flags=FLAG_REFERENCE_TREE)
-    assert np.array_equal(g, b) and st.rays == sb.rays
+    assert st.regen == 1 and st.waves_per_simd == 4  # the large-scene default (PT_WIDE_SCENE_MB)
+    m, sm = render(cfg, tris, nodes, hdr, flags=FLAG_MEGAKERNEL)
+    assert sm.regen == 0 and sm.waves_per_simd == 3
+    b, sb = render(cfg, tris, nodes, hdr, flags=FLAG_MEGAKERNEL | FLAG_REFERENCE_TREE)
+    assert np.array_equal(g, m) and np.array_equal(m, b) and sm.rays == sb.rays
     px = parity.sample_pixels(cfg.width, cfg.height, 2000, seed=5)
     s = parity.assert_parity(g[px[:, 1], px[:, 0]], oracle_pixels(cfg, tris, nodes, hdr, px), "c5/binned")
     print("c5 binned", s, "rays", st.rays)

@@ -211,9 +211,10 @@ def test_tile_order_does_not_change_the_image(c4):
 
 def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
     """A scene past PT_WIDE_SCENE_MB (216k triangles here, like c5's heightfield + teapot)
-    runs the MIS megakernel compiled for 3 waves/SIMD; its pixels meet the oracle's under the
-    same tolerance as test_render_parity, and the runtime tree gives the uploaded tree's image."""
-    from opengl_ray_tracing_amd import FLAG_REFERENCE_TREE
+    runs the MIS path-regeneration kernel compiled for 4 waves/SIMD by default, and the MIS
+    megakernel compiled for 3 with FLAG_MEGAKERNEL; its pixels meet the oracle's under the
+    same tolerance as test_render_parity, and every kernel and tree gives the same image."""
+    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_REFERENCE_TREE
     s = scenes.scene_c3()
     v, i = scenes.heightfield(330)
     s.add_mesh(v, i, scenes.Material(baseColor=(0.6, 0.6, 0.65), roughness=0.4, metallic=0.2, specular=0.5),
@@ -225,9 +226,14 @@ def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
     hdr = scenes.load_hdr(scenes.HDR_FILES[cfg.env])
     w, h, mb = 160, 90, 4
     g, st = render_gpu(cfg, tris, nodes, hdr, frames=2, max_bounce=mb, w=w, h=h)
-    assert st.waves_per_simd == 3
-    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=2, max_bounce=mb, w=w, h=h, flags=FLAG_REFERENCE_TREE)
-    assert np.array_equal(g, b) and st.rays == sb.rays
+    assert st.regen == 1 and st.waves_per_simd == 4
+    m, sm = render_gpu(cfg, tris, nodes, hdr, frames=2, max_bounce=mb, w=w, h=h, flags=FLAG_MEGAKERNEL)
+    assert sm.regen == 0 and sm.waves_per_simd == 3
+    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=2, max_bounce=mb, w=w, h=h,
+                       flags=FLAG_MEGAKERNEL | FLAG_REFERENCE_TREE)
+    assert np.array_equal(g, m) and np.array_equal(m, b) and sm.rays == sb.rays
+    # regeneration skips BRDF rays whose pdf is 0 (IS:816 discards them after tracing)
+    assert sm.rays >= st.rays >= 0.95 * sm.rays
     px = parity.sample_pixels(w, h, w * h, seed=3)
     o, _ = render_oracle(cfg, tris, nodes, hdr, px, frames=2, max_bounce=mb, w=w, h=h)
     parity.assert_parity(g[px[:, 1], px[:, 0]], o[px[:, 1], px[:, 0]], "wide/mis")

@@ -12,7 +12,8 @@ Reads gpurun_out/prof_<tag>_<cfg>/ and writes, under profiles/<tag>/:
 bench.py reads counters.json (--counters) and divides each resource's per-launch
 work by its own live kernel time.
 
-The bench kernel is the culling frame kernel renderKernel<I, true, false[, W]>.
+The bench kernel is the culling frame kernel renderKernel<I, true, false[, W]>
+(or, for large Disney/MIS scenes, the path-regeneration kernel regenKernel<I, true[, W]>).
 bench.py renders PROBE_FRAMES policy-probe frames, then W warmup and K timed
 frames of it, so its timed dispatches are numbers [PROBE+W, PROBE+W+K) in
 dispatch order (the fetch-counting kernel, renderKernel<I, false, true>, and
@@ -37,7 +38,7 @@ OUT = ROOT / "gpurun_out"
 PROBE = 14
 TRACE_RUN = (5, 30)    # tools/gpu_profile.sh: --warmup 5 --steps 30 under --kernel-trace
 COUNTER_RUN = (2, 10)  # --warmup 2 --steps 10 under each --pmc pass
-BENCH_KERNEL = re.compile(r"renderKernel<\d+, true, false(, \d+)?>")
+BENCH_KERNEL = re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true(, \d+)?>")
 
 
 def one(pattern: str) -> Path:
