@@ -643,6 +643,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   __shared__ float4 s_nodes[LDS_NODES * 4];
   {
     const float4* src = p.scene.fast ? p.scene.fbvh : p.scene.bvh;  // the tree traversed first
+    // the copy's size from the staged tree's own record kind (never the other tree's: DESIGN.md §8)
     const int n = p.scene.fast ? p.scene.fnTop * nodeF4<FAST_KIND>() : p.scene.nTop * 4;
     for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
   }
