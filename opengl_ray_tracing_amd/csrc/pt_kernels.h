@@ -88,6 +88,7 @@ constexpr int PKT_DEPTH = 128;    // camera-ray packet stack entries per wave (L
 constexpr int PAIR_F4 = 7;        // float4 per pair record (26 floats: p1, p2, p3, Ng, w of two triangles)
 constexpr int HIT_F4 = 4;         // float4 per hit record (SceneView::hitRec)
 constexpr int MAT_F4 = 5;         // float4 per material (SceneView::mats)
+constexpr int W4_F4 = 8;          // float4 per 4-wide node (SceneView::fbvh4), one 128-byte line
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;
 constexpr int MAX_LEAF = 1 << LEAF_CNT_BITS;
@@ -117,6 +118,10 @@ struct SceneView {
   const float4* fpairs;
   const int* fastTri;
   int fRoot, fnTop;
+  // the same tree collapsed to 4-wide nodes (pt_runtime.cpp encodeWide4; pt_trace.h
+  // traceRay4): W4_F4 float4 per node, breadth-first ids, leaves as in fbvh; null = none
+  const float4* fbvh4;
+  int f4Root, f4nTop;
   // reference facts: each triangle's reference leaf (-1 = none) and that leaf's
   // box (lo, hi), every reference node's parent and box (lo, hi)
   const int* refLeafOf;

@@ -223,8 +223,10 @@ __device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int
   return false;
 }
 
-// WAVES > 0: compiled for that many waves per SIMD (large scenes, pt_runtime.cpp renderOne)
-template <int INTEG, bool CULL, int WAVES = 0>
+// WAVES > 0: compiled for that many waves per SIMD (large scenes, pt_runtime.cpp renderOne).
+// W4: rays walk the 4-wide runtime tree when p.scene.fast (pt_trace.h traceRay4), results
+// checked against the uploaded tree and retraced through it on a tie or an unreachable hit.
+template <int INTEG, bool CULL, int WAVES = 0, bool W4 = false>
 __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U)) void regenKernel(
     RenderParams p) {
   __shared__ int s_stack[REGEN_LDS_STACK * BLOCK];
@@ -235,7 +237,12 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   // the top of the uploaded tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
   __shared__ float4 s_nodes[LDS_NODES * 4];
-  for (int i = threadIdx.x; i < p.scene.nTop * 4; i += BLOCK) s_nodes[i] = p.scene.bvh[i];
+  {
+    const bool w4 = W4 && p.scene.fast;
+    const float4* src = w4 ? p.scene.fbvh4 : p.scene.bvh;
+    const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.nTop * 4;  // the staged tree's own record size
+    for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
+  }
   __syncthreads();
   const float4* top = s_nodes;
 #else
@@ -283,8 +290,20 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
     if (__ballot(active) == 0) break;
     if (!active) continue;
     float t;
-    const int tri = traceRay<false, CULL, false, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(
-        p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW, top);
+    int tri;
+    if (W4 && p.scene.fast) {
+      bool tie = false;
+      const int pos = traceRay4<CULL, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(p.scene, s.o, s.d, t, st, C,
+                                                                                      s.kind == K_SHADOW, top, &tie);
+      tri = pos >= 0 ? p.scene.fastTri[pos] : -1;
+      if (tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t))) {
+        C.rays--;  // the same ray, counted once
+        tri = traceRay<false, CULL, false>(p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW);
+      }
+    } else {
+      tri = traceRay<false, CULL, false, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(
+          p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW, top);
+    }
     V3 color;
     if (!advance<INTEG>(p, s, tri, t, color)) {
       writeAccum(p, s.px, s.py, color);
@@ -296,12 +315,13 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
 
 template <int I>
 static const void* regenFn(bool cull, bool wide) {
-  if (wide && I != 0) return (const void*)regenKernel<I, true, WIDE_REGEN_WAVES>;
+  if (wide && I != 0) return (const void*)regenKernel<I, true, WIDE_REGEN_WAVES, true>;
   return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
 }
 template <int I>
 static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, bool wide) {
-  if (wide && cull && I != 0) hipLaunchKernelGGL((regenKernel<I, true, WIDE_REGEN_WAVES>), dim3(grid), dim3(BLOCK), 0, s, p);
+  if (wide && cull && I != 0)
+    hipLaunchKernelGGL((regenKernel<I, true, WIDE_REGEN_WAVES, true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else hipLaunchKernelGGL((regenKernel<I, false>), dim3(grid), dim3(BLOCK), 0, s, p);
   return hipGetLastError();

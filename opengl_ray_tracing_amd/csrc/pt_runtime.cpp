@@ -84,6 +84,10 @@ struct pt_ctx {
   float4* d_refBox = nullptr;
   float4* d_leafBox = nullptr;
   int fRoot = REF_NONE, fnDev = 0, fDepth = 0;
+  // the same tree collapsed to 4-wide nodes (encodeWide4; the large-scene regen kernel)
+  float4* d_fbvh4 = nullptr;
+  bool fast4Ready = false;
+  int f4Root = REF_NONE, f4nDev = 0, f4Depth = 0;
   // the last pt_upload_scene (pt_frame_stats upload_ms, accel_*)
   float uploadMs = 0.0f, accelMs = 0.0f;
   int accelDevice = -1, accelNodes = 0, accelDepth = 0;
@@ -356,7 +360,7 @@ void pt_destroy(pt_ctx* ctx) {
   (void)hipSetDevice(ctx->cfg.device_id);
   if (ctx->own) (void)hipStreamSynchronize(ctx->own);
   dfree(ctx->d_geo); dfree(ctx->d_hit); dfree(ctx->d_mats); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
-  dfree(ctx->d_fbvh); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri); dfree(ctx->d_refLeafOf);
+  dfree(ctx->d_fbvh); dfree(ctx->d_fbvh4); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri); dfree(ctx->d_refLeafOf);
   dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
@@ -563,6 +567,116 @@ static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, floa
   return "";
 }
 
+// The runtime tree (reference encoding, 12 f32 per node, root 1) collapsed to
+// 4-wide nodes (pt_trace.h traceRay4): each wide node takes a binary node's two
+// children and keeps replacing its internal child of largest surface area by
+// that child's two children until it has four (or only leaves). Wide nodes get
+// breadth-first ids (the first ones are the top the kernels stage in LDS); the
+// children's boxes are widened like encodeWideTree's; leaves keep their
+// references into the pair records. depth: wide levels (root = 1).
+static void encodeWide4(const float* nodes, int nNodes, int nTri, float inflate, float inflateAbs,
+                        std::vector<float4>& out, int& rootRef, int& nDev, int& depth) {
+  auto N = [&](int k, int f) { return nodes[(size_t)k * 12 + f]; };
+  auto isLeaf = [&](int k) { return N(k, 3) > 0.0f; };
+  auto area = [&](int k) {
+    const double dx = N(k, 9) - N(k, 6), dy = N(k, 10) - N(k, 7), dz = N(k, 11) - N(k, 8);
+    return dx * dy + dx * dz + dy * dz;
+  };
+  auto leafRef = [&](int k) {
+    return (int)~(((uint32_t)(int)N(k, 4) << LEAF_CNT_BITS) | (uint32_t)((int)N(k, 3) - 1));
+  };
+  out.clear();
+  nDev = 0;
+  depth = 1;
+  if (nNodes < 2 || isLeaf(1)) {
+    rootRef = nNodes >= 2 ? leafRef(1) : REF_NONE;
+    out.assign(W4_F4, make_float4(0, 0, 0, 0));
+    return;
+  }
+  std::vector<int> queue{1}, level{1};  // binary ids of the wide nodes, breadth-first, and their levels
+  std::vector<std::array<int, 4>> kids;
+  for (size_t q = 0; q < queue.size(); q++) {
+    const int b = queue[q];
+    std::array<int, 4> k = {(int)N(b, 0), (int)N(b, 1), 0, 0};
+    int n = 2;
+    while (n < 4) {
+      int pick = -1;
+      double pa = -1.0;
+      for (int i = 0; i < n; i++)
+        if (!isLeaf(k[i]) && area(k[i]) > pa) { pa = area(k[i]); pick = i; }
+      if (pick < 0) break;
+      const int c = k[pick];
+      k[pick] = (int)N(c, 0);
+      k[n++] = (int)N(c, 1);
+    }
+    for (int i = n; i < 4; i++) k[i] = 0;
+    for (int i = 0; i < n; i++)
+      if (!isLeaf(k[i])) {
+        queue.push_back(k[i]);
+        level.push_back(level[q] + 1);
+        depth = std::max(depth, level[q] + 1);
+      }
+    kids.push_back(k);
+  }
+  nDev = (int)queue.size();
+  std::vector<int> wideId(nNodes, -1);
+  for (int i = 0; i < nDev; i++) wideId[queue[i]] = i;
+  out.assign((size_t)nDev * W4_F4, make_float4(0, 0, 0, 0));
+  for (int w = 0; w < nDev; w++) {
+    float lo[3][4], hi[3][4];
+    int ref[4];
+    for (int i = 0; i < 4; i++) {
+      const int c = kids[w][i];
+      if (c <= 0) {
+        ref[i] = REF_NONE;
+        for (int a = 0; a < 3; a++) { lo[a][i] = INFINITY; hi[a][i] = -INFINITY; }
+        continue;
+      }
+      ref[i] = isLeaf(c) ? leafRef(c) : wideId[c];
+      for (int a = 0; a < 3; a++) {
+        const float l = N(c, 6 + a), h = N(c, 9 + a);
+        const float e = inflate * (std::fabs(l) + std::fabs(h) + (h - l)) + inflateAbs + 1e-30f;
+        lo[a][i] = l - e;
+        hi[a][i] = h + e;
+      }
+    }
+    float4* r = &out[(size_t)w * W4_F4];
+    for (int a = 0; a < 3; a++) {
+      r[a] = make_float4(lo[a][0], lo[a][1], lo[a][2], lo[a][3]);
+      r[3 + a] = make_float4(hi[a][0], hi[a][1], hi[a][2], hi[a][3]);
+    }
+    float fr[4];
+    std::memcpy(fr, ref, sizeof(fr));
+    r[6] = make_float4(fr[0], fr[1], fr[2], fr[3]);
+  }
+  rootRef = 0;
+  (void)nTri;
+}
+
+// the device builder's nodes (pt_build.hip BuildNode, breadth-first from 0) in the
+// reference encoding (BVHNode_encoded, main.cpp:69-73): build node k is node k + 1
+static std::vector<float> refNodes(const std::vector<BuildNode>& bn, int leafSize) {
+  const int M = (int)bn.size();
+  std::vector<float> out((size_t)(M + 1) * 12, 0.0f);
+  for (int k = 0; k < M; k++) {
+    const BuildNode& b = bn[k];
+    float* o = out.data() + 12 * (size_t)(k + 1);
+    int start, count, left, right;
+    std::memcpy(&start, &b.lo.w, 4);
+    std::memcpy(&count, &b.hi.w, 4);
+    std::memcpy(&left, &b.clo.w, 4);
+    std::memcpy(&right, &b.chi.w, 4);
+    const bool leaf = count <= leafSize;
+    o[0] = leaf ? 0.0f : (float)(left + 1);
+    o[1] = leaf ? 0.0f : (float)(right + 1);
+    o[3] = leaf ? (float)count : 0.0f;
+    o[4] = leaf ? (float)start : 0.0f;
+    o[6] = b.lo.x; o[7] = b.lo.y; o[8] = b.lo.z;
+    o[9] = b.hi.x; o[10] = b.hi.y; o[11] = b.hi.z;
+  }
+  return out;
+}
+
 // pair records: position i holds triangles order[i] (x) and order[i + 1] (y,
 // zeros past the last), PAIR_F4 float4 each (pt_trace.h pairTest)
 static void buildPairs(const std::vector<float4>& geo, const int* order, int nTri, std::vector<float4>& pairs) {
@@ -595,6 +709,7 @@ struct SceneHost {
   bool deviceBuild = false;  // the tree itself is built on each device (pt_build.hip) by uploadScene
   float accelMs = 0.0f;      // host build time (deviceBuild false)
   int accelNodes = 0;
+  std::vector<float> accelRef;  // host build: its nodes in the reference encoding (encodeWide4)
   WideTree fastTree;
   std::vector<float4> fpairs, refBox, leafBox;
   std::vector<int> order, leafOf, parent;
@@ -669,6 +784,7 @@ static void prepareAccel(const float* tris, int nTri, const float* nodes, int nN
   std::vector<float> an;
   if (pt::buildAccel(tris, nTri, PT_ACCEL_LEAF, an, h.order) < 0 || an.size() / 12 >= (1u << 24)) return;
   h.accelNodes = (int)(an.size() / 12) - 1;
+  h.accelRef = an;
 
   // widened by 1e-5 of each box's own magnitude plus 3e-5 of the scene's: above
   // the rounding of a slab test (~1.2e-7 x the origin-box distance) for ray origins
@@ -758,6 +874,8 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   ctx->depth = h.ref.depth;
   ctx->maxStack = h.ref.depth + 1;
   ctx->fastReady = false;
+  ctx->fast4Ready = false;
+  std::vector<float> accelRef;  // the device-built tree in the reference encoding
   ctx->accelDevice = -1;
   ctx->accelMs = 0.0f;
   ctx->accelNodes = ctx->accelDepth = 0;
@@ -771,11 +889,19 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
     AccelBuild ab;
     hipError_t e = buildAccelDevice(ctx->d_geo, h.nTri, PT_ACCEL_LEAF, 1e-5f, 3e-5f, ab, ctx->stream);
     if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("device tree build: ") + hipGetErrorString(e));
-    dfree(ab.nodes);
     if (ab.nNodes + 1 >= (1 << 24)) {  // as the host path: no runtime tree of 2^24 nodes or more
       freeAccelBuild(ab);
       return PT_OK;
     }
+    // its nodes on the host, for the 4-wide collapse
+    std::vector<BuildNode> bn(ab.nNodes);
+    e = hipMemcpy(bn.data(), ab.nodes, bn.size() * sizeof(BuildNode), hipMemcpyDeviceToHost);
+    dfree(ab.nodes);
+    if (e != hipSuccess) {
+      freeAccelBuild(ab);
+      return fail(ctx, PT_E_HIP, std::string("device tree download: ") + hipGetErrorString(e));
+    }
+    accelRef = refNodes(bn, PT_ACCEL_LEAF);
     dfree(ctx->d_fbvh);
     dfree(ctx->d_fpairs);
     dfree(ctx->d_fastTri);
@@ -800,6 +926,19 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
     ctx->accelNodes = h.accelNodes;
   }
   ctx->accelDepth = ctx->fDepth;
+  // the 4-wide collapse (the large-scene regen kernel's tree), widened like the binary records
+  {
+    const std::vector<float>& an = h.deviceBuild ? accelRef : h.accelRef;
+    const int nn = (int)(an.size() / 12);
+    float scale = 0.0f;  // the scene's largest coordinate magnitude: the root box's
+    for (int k = 6; k < 12 && nn > 1; k++) scale = std::max(scale, std::fabs(an[12 + k]));
+    std::vector<float4> w4;
+    encodeWide4(an.data(), nn, h.nTri, 1e-5f, 3e-5f * scale, w4, ctx->f4Root, ctx->f4nDev, ctx->f4Depth);
+    if ((rc = upload(ctx, &ctx->d_fbvh4, w4))) return rc;
+    ctx->fast4Ready = true;
+    // a visit pushes up to three children: the traversal stack needs 3 entries per wide level
+    ctx->maxStack = std::max(ctx->maxStack, 3 * ctx->f4Depth + 2);
+  }
   ctx->sceneVersion++;  // camera-ray bins are rebuilt for the new triangles
   ctx->maxStack = std::max(ctx->maxStack, ctx->fDepth + 1);
   ctx->fastReady = true;
@@ -860,24 +999,8 @@ int pt_build_bvh_device(pt_ctx* ctx, const float* tris, int nTri, int leafSize, 
   freeAccelBuild(ab);
   if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("device tree download: ") + hipGetErrorString(e));
   if (M + 1 > maxNodes) return fail(ctx, PT_E_INVALID, "nodes_out holds fewer than *nNodes_out nodes");
-  // the reference encoding (BVHNode_encoded, main.cpp:69-73, 688-716): build node k is node k + 1
-  std::memset(nodes_out, 0, sizeof(float) * 12 * (size_t)(M + 1));
-  for (int k = 0; k < M; k++) {
-    const BuildNode& b = bn[k];
-    float* o = nodes_out + 12 * (size_t)(k + 1);
-    int start, count, left, right;
-    std::memcpy(&start, &b.lo.w, 4);
-    std::memcpy(&count, &b.hi.w, 4);
-    std::memcpy(&left, &b.clo.w, 4);
-    std::memcpy(&right, &b.chi.w, 4);
-    const bool leaf = count <= leafSize;
-    o[0] = leaf ? 0.0f : (float)(left + 1);
-    o[1] = leaf ? 0.0f : (float)(right + 1);
-    o[3] = leaf ? (float)count : 0.0f;
-    o[4] = leaf ? (float)start : 0.0f;
-    o[6] = b.lo.x; o[7] = b.lo.y; o[8] = b.lo.z;
-    o[9] = b.hi.x; o[10] = b.hi.y; o[11] = b.hi.z;
-  }
+  const std::vector<float> ref = refNodes(bn, leafSize);
+  std::memcpy(nodes_out, ref.data(), ref.size() * sizeof(float));
   return PT_OK;
 }
 
@@ -1069,6 +1192,9 @@ static SceneView sceneView(const pt_ctx* ctx) {
   s.fastTri = ctx->d_fastTri;
   s.fRoot = ctx->fRoot;
   s.fnTop = std::min(LDS_NODES, ctx->fnDev);
+  s.fbvh4 = ctx->d_fbvh4;
+  s.f4Root = ctx->f4Root;
+  s.f4nTop = std::min(LDS_NODES * 4 / W4_F4, ctx->f4nDev);  // the LDS copy holds LDS_NODES * 4 float4
   s.refLeafOf = ctx->d_refLeafOf;
   s.refParent = ctx->d_refParent;
   s.refBox = ctx->d_refBox;
@@ -1395,6 +1521,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   bool useFast = false;
   const int splitPct = probePolicy(ctx, frameCounter, ordered,
                                    !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast);
+  // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
+  if (regen && wide && ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE)) useFast = true;
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;

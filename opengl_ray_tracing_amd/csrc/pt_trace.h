@@ -381,6 +381,121 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
   return best;
 }
 
+// ----------------------------------------------------------------- 4-wide runtime tree
+// The runtime tree collapsed to 4-wide nodes (pt_runtime.cpp encodeWide4): per
+// node {lo.x of children 0..3}, {lo.y}, {lo.z}, {hi.x}, {hi.y}, {hi.z}, {refs},
+// {-}: 128 bytes, one line. A visit tests the four (widened) child boxes with
+// fused slabs, visits the nearest hit child next and pushes the others far to
+// near: about half the dependent node fetches of the binary walk, for
+// memory-latency-bound walks of large scenes (the regen kernel on scenes past
+// PT_WIDE_SCENE_MB). Results are checked exactly like the binary runtime
+// tree's (the order of visits only matters for exact-t ties, which are
+// flagged: refReachable, the retrace in the reference order).
+constexpr float PT_INF_KEY = __builtin_huge_valf();  // sort key of a missed child (every entry t is finite)
+__device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
+  const bool s = kb < ka;
+  const float k = s ? kb : ka;
+  const int r = s ? rb : ra;
+  kb = s ? ka : kb;
+  rb = s ? ra : rb;
+  ka = k;
+  ra = r;
+}
+template <bool CULL, class StackType, bool LDSTOP>
+__device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
+                                         bool anyRT, const float4* top, bool* tie) {
+  const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const FusedRay fr = fusedRay(o, inv);
+  const f32x2 ix = {fr.inv.x, fr.inv.x}, iy = {fr.inv.y, fr.inv.y}, iz = {fr.inv.z, fr.inv.z};
+  const f32x2 ox = {fr.noi.x, fr.noi.x}, oy = {fr.noi.y, fr.noi.y}, oz = {fr.noi.z, fr.noi.z};
+  float tbest = PT_INF;
+  int best = -1;
+  int ref = S.f4Root;
+  int leaf = REF_NONE;
+  st.reset();
+  C.rays++;
+  while (true) {
+    while (ref >= 0) {
+      const float4* nd = S.fbvh4 + (size_t)W4_F4 * ref;
+      if (LDSTOP && ref < S.f4nTop) nd = top + W4_F4 * ref;
+      const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+      float key[4];
+      int r[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+      const float lim = tbest + 1e-3f * fmaxf(1.0f, tbest);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {  // children (0, 1) and (2, 3) as packed pairs
+        const f32x2 Lx = h ? f32x2{lx.z, lx.w} : f32x2{lx.x, lx.y}, Ly = h ? f32x2{ly.z, ly.w} : f32x2{ly.x, ly.y};
+        const f32x2 Lz = h ? f32x2{lz.z, lz.w} : f32x2{lz.x, lz.y}, Hx = h ? f32x2{hx.z, hx.w} : f32x2{hx.x, hx.y};
+        const f32x2 Hy = h ? f32x2{hy.z, hy.w} : f32x2{hy.x, hy.y}, Hz = h ? f32x2{hz.z, hz.w} : f32x2{hz.x, hz.y};
+        const f32x2 fx = __builtin_elementwise_fma(Hx, ix, ox), fy = __builtin_elementwise_fma(Hy, iy, oy),
+                    fz = __builtin_elementwise_fma(Hz, iz, oz);
+        const f32x2 nx = __builtin_elementwise_fma(Lx, ix, ox), ny = __builtin_elementwise_fma(Ly, iy, oy),
+                    nz = __builtin_elementwise_fma(Lz, iz, oz);
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int c = 2 * h + e;
+          const float t1 = fminf(fmaxf(fx[e], nx[e]), fminf(fmaxf(fy[e], ny[e]), fmaxf(fz[e], nz[e])));
+          const float t0 = fmaxf(fminf(fx[e], nx[e]), fmaxf(fminf(fy[e], ny[e]), fminf(fz[e], nz[e])));
+          bool hit = r[c] != REF_NONE && t1 >= t0 && t1 > 0.0f;
+          if (CULL) hit = hit && !(t0 > lim);
+          key[c] = hit ? t0 : PT_INF_KEY;
+        }
+      }
+      // nearest first: sort the four (entry t, ref) pairs, misses last
+      cswap(key[0], r[0], key[1], r[1]);
+      cswap(key[2], r[2], key[3], r[3]);
+      cswap(key[0], r[0], key[2], r[2]);
+      cswap(key[1], r[1], key[3], r[3]);
+      cswap(key[1], r[1], key[2], r[2]);
+      int next;
+      if (key[0] < PT_INF_KEY) {
+        if (key[3] < PT_INF_KEY) st.push(r[3]);
+        if (key[2] < PT_INF_KEY) st.push(r[2]);
+        if (key[1] < PT_INF_KEY) st.push(r[1]);
+        next = r[0];
+      } else {
+        next = st.sp > 0 ? st.pop() : REF_NONE;
+      }
+      if (isLeafRef(next) && leaf == REF_NONE) {  // park it, walk on (traceRay's while-while)
+        leaf = next;
+        next = st.sp > 0 ? st.pop() : REF_NONE;
+      }
+      ref = next;
+      if (__ballot(leaf == REF_NONE) == 0) break;
+    }
+    if (leaf == REF_NONE && isLeafRef(ref)) {
+      leaf = ref;
+      ref = st.sp > 0 ? st.pop() : REF_NONE;
+    }
+    if (leaf == REF_NONE) break;
+    const uint32_t v = ~(uint32_t)leaf;
+    const int start = (int)(v >> LEAF_CNT_BITS);
+    const int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
+    leaf = REF_NONE;
+    for (int k = 0; k < cnt; k += 2) {
+      const int i = start + k;
+      const bool second = k + 1 < cnt;
+      float t0, t1;
+      bool g0, g1;
+      pairTest(S.fpairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1);
+      if (g0 && t0 == tbest) *tie = true;
+      if (g0 && t0 < tbest) {
+        tbest = t0;
+        best = i;
+        if (anyRT) { tOut = tbest; return best; }
+      }
+      if (g1 && second && t1 == tbest) *tie = true;
+      if (g1 && second && t1 < tbest) {
+        tbest = t1;
+        best = i + 1;
+        if (anyRT) { tOut = tbest; return best; }
+      }
+    }
+  }
+  tOut = tbest;
+  return best;
+}
+
 // ----------------------------------------------------------------- reference-exact results
 // Reference-exact results through the runtime's tree. The reference's closest
 // hit is the first, in its traversal order, of the triangles with the least t
