@@ -32,7 +32,10 @@ constexpr int WIDE_WAVES = 3;
 // (c5: 16 bounces) a lane that takes a new pixel when its path ends beats the
 // lock-step megakernel, whose waves last as long as their longest path (c5: 10.0
 // -> 9.2 ms; on the L2-resident c4 the regen kernel is 3.6x slower)
-constexpr int WIDE_REGEN_WAVES = 4;
+#ifndef PT_WIDE_REGEN_WAVES
+#define PT_WIDE_REGEN_WAVES 4
+#endif
+constexpr int WIDE_REGEN_WAVES = PT_WIDE_REGEN_WAVES;
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
@@ -75,6 +78,13 @@ constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
 #define PT_QUANT_NODES 0  // 1: the runtime tree's node records quantized to 8 bits per plane (measured slower: DESIGN.md)
 #endif
 constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
+#ifndef PT_WIDE4
+// the megakernel's traced rays walk the runtime tree collapsed to 4-wide nodes (pt_trace.h
+// traceRay4; camera rays keep their bins and the binary tree's packets): 2 = with the 4-wide
+// tree's top 64 nodes in LDS (c2 0.408 -> 0.376 ms, c4 0.498 -> 0.477, c3 0.273 -> 0.262),
+// 1 = without (c3 0.257, c2 0.380), 0 = the binary runtime tree
+#define PT_WIDE4 2
+#endif
 #ifndef PT_FUSED_SLABS
 #define PT_FUSED_SLABS 1  // the runtime tree's slab tests as packed FMAs (pt_trace.h visitNodeF)
 #endif

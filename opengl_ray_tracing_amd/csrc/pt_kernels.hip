@@ -38,6 +38,16 @@ struct Tracer {
   // closest hit: the triangle (-1 = miss) and its t. With S.fast, through the
   // runtime's tree and checked against the reference's (pt_trace.h refReachable).
   __device__ __forceinline__ int trace(V3 o, V3 d, float& t) {
+    if (PT_WIDE4 && !COUNT && S.fast) {  // the 4-wide runtime tree (PT_WIDE4), checked as the binary one
+      bool tie = false;
+      const int pos = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, false, top, &tie);
+      int tri = pos >= 0 ? S.fastTri[pos] : -1;
+      if (tie || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
+        C.rays--;
+        tri = traceRay<false, CULL, false, Stack>(S, o, d, t, st, C);
+      }
+      return tri;
+    }
     if (!COUNT && S.fast) {
       bool tie = false;
       const SceneView F = fastView(S);
@@ -60,6 +70,14 @@ struct Tracer {
   }
   __device__ __forceinline__ bool occluded(V3 o, V3 d) {
     float t;
+    if (PT_WIDE4 && !COUNT && S.fast) {
+      bool tie = false;
+      const int pos = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, true, top, &tie);
+      if (pos < 0) return false;
+      if (refReachable(S, S.fastTri[pos], o, d, t)) return true;
+      C.rays--;
+      return traceRay<true, CULL, false, Stack>(S, o, d, t, st, C) >= 0;
+    }
     if (!COUNT && S.fast) {
       const SceneView F = fastView(S);
       const int pos = traceRay<true, CULL, false, Stack, (LDS_NODES > 0), false, FAST_KIND>(F, o, d, t, st, C, false, top);
@@ -301,7 +319,8 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
       tri = tr.trace(eye, dir, t);
     }
   } else if (p.scene.fast) {  // through the runtime's tree, checked against the reference's
-    const int pos = tracePacket<CULL, FAST_KIND>(fastView(p.scene), eye, dir, valid, t, tie, pstack, C, top);
+    const int pos = tracePacket<CULL, FAST_KIND>(fastView(p.scene), eye, dir, valid, t, tie, pstack, C,
+                                                  PT_WIDE4 == 2 ? nullptr : top);
     tri = pos >= 0 ? p.scene.fastTri[pos] : -1;
     if (valid && (tie || (tri >= 0 && !refReachable(p.scene, tri, eye, dir, t)))) {
       C.rays--;  // the same ray, counted once
@@ -642,9 +661,10 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
 #if PT_LDS_NODES > 0
   __shared__ float4 s_nodes[LDS_NODES * 4];
   {
-    const float4* src = p.scene.fast ? p.scene.fbvh : p.scene.bvh;  // the tree traversed first
+    const bool w4 = PT_WIDE4 == 2 && !COUNT && p.scene.fast;  // the 4-wide tree's top
+    const float4* src = w4 ? p.scene.fbvh4 : p.scene.fast ? p.scene.fbvh : p.scene.bvh;  // the tree traversed first
     // the copy's size from the staged tree's own record kind (never the other tree's: DESIGN.md §8)
-    const int n = p.scene.fast ? p.scene.fnTop * nodeF4<FAST_KIND>() : p.scene.nTop * 4;
+    const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.fast ? p.scene.fnTop * nodeF4<FAST_KIND>() : p.scene.nTop * 4;
     for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
   }
   __syncthreads();
@@ -749,6 +769,7 @@ __global__ __launch_bounds__(BLOCK) void traceKernel(TraceParams p) {
   SceneView S = p.scene;  // no LDS copy of the top of the tree here
   S.nTop = 0;
   S.fnTop = 0;
+  S.f4nTop = 0;
   Tracer<CULL, false> tr{S, st, C, nullptr};  // the runtime's tree when S.fast (reference-exact)
   for (size_t k = gtid; k < (size_t)p.n; k += (size_t)gridDim.x * BLOCK) {
     const float* r = p.rays + 6 * k;
