@@ -194,7 +194,8 @@ int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out);
 
 /* Multi-process tile exchange (one process per GPU, pt_config.tile_rank/tile_world):
  * pack this rank's owned pixels into a contiguous device buffer (count =
- * pt_owned_pixel_count), and unpack another rank's packed pixels into this
+ * pt_owned_pixel_count slots of 3 f32: r, g, b -- a rendered pixel's alpha is
+ * always 1, and unpack writes 1), and unpack another rank's packed pixels into this
  * context's accumulation. Pointers are device memory; the caller moves the
  * packed buffers (RCCL gather over xGMI). Not for n_devices > 1 contexts, which
  * gather inside pt_render_frame. */

@@ -282,9 +282,11 @@ int regenLdsStack();
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s);
-hipError_t launchPack(const PackParams& p, const float4* accum, float4* packed, hipStream_t s);
+// PACK_F floats (r, g, b) per packed slot
+constexpr int PACK_F = 3;
+hipError_t launchPack(const PackParams& p, const float4* accum, float* packed, hipStream_t s);
 hipError_t launchFmath(int fn, const float* x, const float* y, int n, float* out, hipStream_t s);
-hipError_t launchUnpack(const PackParams& p, float4* accum, const float4* packed, hipStream_t s);
+hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s);
 // the running-mean update of a pipelined frame over the rank's owned pixels (PackParams
 // mapping): accum = mix(accum, col, 1 / (frameCounter + 1)) (IS:868-871, pass2.fsh:15)
 hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s);

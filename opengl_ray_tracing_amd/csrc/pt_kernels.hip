@@ -811,17 +811,23 @@ __device__ __forceinline__ bool packedPixel(const PackParams& p, long k, int& px
   py = gy * p.shardSize + within / p.shardSize;
   return px < p.width && py < p.height;
 }
-__global__ void packKernel(PackParams p, const float4* accum, float4* packed) {
+// packed slots are (r, g, b): the running mean's alpha is 1 for every rendered pixel
+// (IS:868-871 writes vec4(color, 1)), so the gather moves 12 bytes per pixel, not 16
+__global__ void packKernel(PackParams p, const float4* accum, float* packed) {
   long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= p.count) return;
   int px, py;
-  packed[k] = packedPixel(p, k, px, py) ? accum[(size_t)py * p.width + px] : make_float4(0, 0, 0, 0);
+  const float4 c = packedPixel(p, k, px, py) ? accum[(size_t)py * p.width + px] : make_float4(0, 0, 0, 0);
+  packed[3 * k] = c.x;
+  packed[3 * k + 1] = c.y;
+  packed[3 * k + 2] = c.z;
 }
-__global__ void unpackKernel(PackParams p, float4* accum, const float4* packed) {
+__global__ void unpackKernel(PackParams p, float4* accum, const float* packed) {
   long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= p.count) return;
   int px, py;
-  if (packedPixel(p, k, px, py)) accum[(size_t)py * p.width + px] = packed[k];
+  if (packedPixel(p, k, px, py))
+    accum[(size_t)py * p.width + px] = make_float4(packed[3 * k], packed[3 * k + 1], packed[3 * k + 2], 1.0f);
 }
 
 // the running mean of a pipelined frame (accumulate's update, deferred to frame order)
@@ -919,7 +925,7 @@ hipError_t launchFmath(int fn, const float* x, const float* y, int n, float* out
   return hipGetLastError();
 }
 
-hipError_t launchPack(const PackParams& p, const float4* accum, float4* packed, hipStream_t s) {
+hipError_t launchPack(const PackParams& p, const float4* accum, float* packed, hipStream_t s) {
   if (p.count <= 0) return hipSuccess;
   hipLaunchKernelGGL(packKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, packed);
   return hipGetLastError();
@@ -929,7 +935,7 @@ hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint
   hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, col, frameCounter);
   return hipGetLastError();
 }
-hipError_t launchUnpack(const PackParams& p, float4* accum, const float4* packed, hipStream_t s) {
+hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s) {
   if (p.count <= 0) return hipSuccess;
   hipLaunchKernelGGL(unpackKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, packed);
   return hipGetLastError();

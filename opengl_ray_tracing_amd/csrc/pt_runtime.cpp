@@ -172,8 +172,8 @@ struct GroupGather {
   struct Peer {
     int dev = 0;
     size_t count = 0;                       // packed pixels (float4) of this rank
-    float4* send[2] = {nullptr, nullptr};   // on the rank's device
-    float4* recv = nullptr;                 // on rank 0's device
+    float* send[2] = {nullptr, nullptr};    // on the rank's device, PACK_F floats per slot
+    float* recv = nullptr;                  // on rank 0's device
     hipStream_t mstream = nullptr;          // the rank's device: RCCL sends
     hipEvent_t packed[2] = {nullptr, nullptr};
     hipEvent_t sent[2] = {nullptr, nullptr};  // the buffer's transfer completed
@@ -1775,7 +1775,7 @@ int pt_pack_owned(pt_ctx* ctx, void* dpacked) {
   if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   PackParams p = packParams(ctx, ctx->cfg.tile_rank, ctx->cfg.tile_world);
-  CK(launchPack(p, ctx->d_accum, reinterpret_cast<float4*>(dpacked), ctx->stream));
+  CK(launchPack(p, ctx->d_accum, reinterpret_cast<float*>(dpacked), ctx->stream));
   return PT_OK;
 }
 
@@ -1785,7 +1785,7 @@ int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked) {
   if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
   PackParams p = packParams(ctx, rank, world);
-  CK(launchUnpack(p, ctx->d_accum, reinterpret_cast<const float4*>(dpacked), ctx->stream));
+  CK(launchUnpack(p, ctx->d_accum, reinterpret_cast<const float*>(dpacked), ctx->stream));
   return PT_OK;
 }
 
@@ -1986,13 +1986,13 @@ static int createGroup(pt_ctx* ctx) {
     P.dev = devs[k];
     P.count = (size_t)packParams(m, k, n).count;
     CK(hipSetDevice(devs[0]));
-    if (P.count) CK(hipMalloc(&P.recv, P.count * sizeof(float4)));
+    if (P.count) CK(hipMalloc(&P.recv, P.count * PACK_F * sizeof(float)));
     // copy mode: the transfer (and its completion event) runs on rank 0's device
     for (int i = 0; i < 2; i++)
       if (g->mode == PT_GATHER_COPY) CK(hipEventCreateWithFlags(&P.sent[i], hipEventDisableTiming));
     CK(hipSetDevice(P.dev));
     for (int i = 0; i < 2; i++) {
-      if (P.count) CK(hipMalloc(&P.send[i], P.count * sizeof(float4)));
+      if (P.count) CK(hipMalloc(&P.send[i], P.count * PACK_F * sizeof(float)));
       CK(hipEventCreateWithFlags(&P.packed[i], hipEventDisableTiming));
       if (g->mode == PT_GATHER_RCCL) CK(hipEventCreateWithFlags(&P.sent[i], hipEventDisableTiming));
     }
@@ -2034,8 +2034,8 @@ static int groupGather(pt_ctx* ctx) {
     for (int k = 1; k < n && e == ncclSuccess; k++) {
       GroupGather::Peer& P = g.peer[k - 1];
       if (!P.count) continue;
-      e = R.send(P.send[i], P.count * 4, ncclFloat32, 0, g.comms[k], P.mstream);
-      if (e == ncclSuccess) e = R.recv(P.recv, P.count * 4, ncclFloat32, k, g.comms[0], g.cstream);
+      e = R.send(P.send[i], P.count * PACK_F, ncclFloat32, 0, g.comms[k], P.mstream);
+      if (e == ncclSuccess) e = R.recv(P.recv, P.count * PACK_F, ncclFloat32, k, g.comms[0], g.cstream);
     }
     ncclResult_t e2 = R.groupEnd();
     if (e == ncclSuccess) e = e2;
@@ -2050,7 +2050,7 @@ static int groupGather(pt_ctx* ctx) {
     for (auto& P : g.peer) {
       if (!P.count) continue;
       CK(hipStreamWaitEvent(g.cstream, P.packed[i], 0));
-      CK(hipMemcpyPeerAsync(P.recv, dev0, P.send[i], P.dev, P.count * sizeof(float4), g.cstream));
+      CK(hipMemcpyPeerAsync(P.recv, dev0, P.send[i], P.dev, P.count * PACK_F * sizeof(float), g.cstream));
       CK(hipEventRecord(P.sent[i], g.cstream));
     }
   }

@@ -94,9 +94,10 @@ class FrameGather:
         self.render_stream = torch.cuda.Stream(device)
         self.comm_stream = torch.cuda.Stream(device) if self.overlap else self.render_stream
         nbuf = 2 if self.overlap else 1
-        self.send = [torch.zeros((self.maxc, 4), dtype=torch.float32, device=device) for _ in range(nbuf)]
+        # packed slots: 3 f32 (r, g, b; pt_pack_owned), 12 bytes per pixel over xGMI
+        self.send = [torch.zeros((self.maxc, 3), dtype=torch.float32, device=device) for _ in range(nbuf)]
         self.sent = [None] * nbuf  # event: the buffer's last gather has completed
-        self.recv = [torch.zeros((self.maxc, 4), dtype=torch.float32, device=device) for _ in range(world)] \
+        self.recv = [torch.zeros((self.maxc, 3), dtype=torch.float32, device=device) for _ in range(world)] \
             if rank == 0 else None
         self.k = 0
         renderer.set_stream(self.render_stream.cuda_stream)
