@@ -416,6 +416,10 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
   C.rays++;
   while (true) {
     while (ref >= 0) {
+      if (PT_WAVE_TRACE) {  // diagnostics build: node-loop iterations (lane, wave)
+        C.nodes++;
+        if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
+      }
       const float4* nd = S.fbvh4 + (size_t)W4_F4 * ref;
       if (LDSTOP && ref < S.f4nTop) nd = top + W4_F4 * ref;
       const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
@@ -473,6 +477,10 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
     const int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
     leaf = REF_NONE;
     for (int k = 0; k < cnt; k += 2) {
+      if (PT_WAVE_TRACE) {  // diagnostics build: leaf-loop iterations (lane, wave)
+        C.tris++;
+        if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
+      }
       const int i = start + k;
       const bool second = k + 1 < cnt;
       float t0, t1;

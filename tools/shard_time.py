@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Per-rank frame time of the screen-tile split, measured on one GPU: rank 0's
+share of an N-way split (its 32x32 tiles t % N == 0) rendered alone, wall ms per
+frame with frames in flight. The N-GPU frame is at least this plus whatever of
+the per-frame gather does not overlap the next frame.
+
+    [PT_VARIANT=<tuning build>] python tools/shard_time.py [config] [N ...]
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    cfg_name = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    worlds = [int(x) for x in sys.argv[2:]] or [1, 2, 4, 8]
+    import os
+
+    import torch  # noqa: F401  (one HIP runtime with torch, as in bench.py)
+    from opengl_ray_tracing_amd import _native
+    if os.environ.get("PT_VARIANT"):  # an in-tree tuning build (tools/tune.py --build)
+        _native.use_variant(os.environ["PT_VARIANT"])
+    from opengl_ray_tracing_amd import Renderer, orbit_camera, scenes
+    cfg, tris, nodes, hdr = scenes.build_config(cfg_name)
+    eye, rot = orbit_camera(*cfg.camera)
+    for n in worlds:
+        with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, tile_rank=0,
+                      tile_world=n) as r:
+            r.upload_scene(tris, nodes)
+            r.upload_env(hdr)
+            for f in range(24):  # policy probe + warmup
+                r.render_frame(eye, rot, f, sync=False)
+            r.synchronize()
+            r.reset_stats()
+            K = 100
+            t0 = time.perf_counter()
+            for f in range(24, 24 + K):
+                r.render_frame(eye, rot, f, sync=False)
+            r.synchronize()
+            ms = 1e3 * (time.perf_counter() - t0) / K
+            st = r.stats()
+        print(json.dumps({"variant": os.environ.get("PT_VARIANT", "base"), "config": cfg_name, "world": n, "rank0_ms_per_frame": round(ms, 4),
+                          "kernel_ms_avg": round(st.kernel_ms_total / max(st.launches, 1), 4),
+                          "rays_per_frame": st.rays // max(st.launches, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
