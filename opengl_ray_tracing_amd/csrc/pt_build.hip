@@ -604,6 +604,84 @@ __global__ void pairsKernel(const float4* geo, const int* order, int n, float4* 
   r[6] = make_float4(a0.w, b0.w, 0.0f, 0.0f);
 }
 
+// ------------------------------------------------------------ 4-wide collapse
+// pt_runtime.cpp encodeWide4 on the device, level by level: every wide node of a
+// level takes its binary node's two children and keeps replacing the internal
+// child of largest surface area (first one on ties, areas in double as on the
+// host) by that child's two children until it has four; the next level's wide
+// nodes are the internal children in (node, child) order, so ids are
+// breadth-first and identical to the host collapse of the same binary tree.
+__device__ __forceinline__ bool bLeaf(const BuildNode& n, int leafSize) { return nodeCount(n) <= leafSize; }
+__device__ __forceinline__ double bArea(const BuildNode& n) {
+  const double dx = (double)n.hi.x - n.lo.x, dy = (double)n.hi.y - n.lo.y, dz = (double)n.hi.z - n.lo.z;
+  return dx * dy + dx * dz + dy * dz;
+}
+__global__ void w4ExpandKernel(const BuildNode* nodes, const int* front, int F, int leafSize, int4* kids, int* cnt) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f > F) return;
+  if (f == F) { cnt[f] = 0; return; }
+  const BuildNode b = nodes[front[f]];
+  int k[4] = {__float_as_int(b.clo.w), __float_as_int(b.chi.w), -1, -1};
+  int n = 2;
+  while (n < 4) {
+    int pick = -1;
+    double pa = -1.0;
+    for (int i = 0; i < n; i++) {
+      const BuildNode c = nodes[k[i]];
+      if (!bLeaf(c, leafSize) && bArea(c) > pa) { pa = bArea(c); pick = i; }
+    }
+    if (pick < 0) break;
+    const BuildNode c = nodes[k[pick]];
+    k[pick] = __float_as_int(c.clo.w);
+    k[n++] = __float_as_int(c.chi.w);
+  }
+  int internal = 0;
+  for (int i = 0; i < n; i++) internal += !bLeaf(nodes[k[i]], leafSize);
+  kids[f] = make_int4(k[0], k[1], k[2], k[3]);
+  cnt[f] = internal;
+}
+// the level's records (wide ids base + f) and the next level's frontier (wide ids base + F + scan)
+__global__ void w4EncodeKernel(const BuildNode* nodes, const int4* kids, const int* scan, int F, int base,
+                               int leafSize, float inflate, float relAbs, float4* out, int* nextFront) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  const BuildNode r0 = nodes[0];
+  const float scale = fmaxf(fmaxf(fmaxf(fabsf(r0.lo.x), fabsf(r0.hi.x)), fmaxf(fabsf(r0.lo.y), fabsf(r0.hi.y))),
+                            fmaxf(fabsf(r0.lo.z), fabsf(r0.hi.z)));
+  const float inflateAbs = relAbs * scale;
+  const int4 kv = kids[f];
+  const int k[4] = {kv.x, kv.y, kv.z, kv.w};
+  float lo[3][4], hi[3][4];
+  int ref[4];
+  int next = scan[f];
+  for (int i = 0; i < 4; i++) {
+    if (k[i] < 0) {
+      ref[i] = REF_NONE;
+      for (int a = 0; a < 3; a++) { lo[a][i] = INFINITY; hi[a][i] = -INFINITY; }
+      continue;
+    }
+    const BuildNode c = nodes[k[i]];
+    if (bLeaf(c, leafSize)) {
+      ref[i] = (int)~(((uint32_t)nodeStart(c) << LEAF_CNT_BITS) | (uint32_t)(nodeCount(c) - 1));
+    } else {
+      nextFront[next] = k[i];
+      ref[i] = base + F + next;
+      next++;
+    }
+    float4 l = make_float4(c.lo.x, c.lo.y, c.lo.z, 0.0f), h = make_float4(c.hi.x, c.hi.y, c.hi.z, 0.0f);
+    widen(l, h, inflate, inflateAbs);
+    lo[0][i] = l.x; lo[1][i] = l.y; lo[2][i] = l.z;
+    hi[0][i] = h.x; hi[1][i] = h.y; hi[2][i] = h.z;
+  }
+  float4* r = out + (size_t)(base + f) * W4_F4;
+  for (int a = 0; a < 3; a++) {
+    r[a] = make_float4(lo[a][0], lo[a][1], lo[a][2], lo[a][3]);
+    r[3 + a] = make_float4(hi[a][0], hi[a][1], hi[a][2], hi[a][3]);
+  }
+  r[6] = make_float4(__int_as_float(ref[0]), __int_as_float(ref[1]), __int_as_float(ref[2]), __int_as_float(ref[3]));
+  r[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
 inline int blocks(long n, int t = 256) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -753,6 +831,72 @@ hipError_t buildAccelDevice(const float4* geo, int nTri, int leafSize, float inf
   if (hostCls) (void)hipHostFree(hostCls);
   if (e != hipSuccess) freeAccelBuild(out);
   return e;
+}
+
+hipError_t collapseWide4Device(const BuildNode* nodes, int nNodes, int leafSize, float inflate, float inflateRelAbs,
+                               float4** out, int* rootRef, int* nDev, int* depth, hipStream_t s) {
+  *out = nullptr;
+  *nDev = 0;
+  *depth = 1;
+  if (nNodes < 1) return hipErrorInvalidValue;
+  BuildNode root;
+  hipError_t e = hipMemcpyAsync(&root, nodes, sizeof(root), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  int rootCount;
+  std::memcpy(&rootCount, &root.hi.w, 4);
+  if (rootCount <= leafSize) {  // one leaf: no wide node
+    int start;
+    std::memcpy(&start, &root.lo.w, 4);
+    *rootRef = (int)~(((uint32_t)start << LEAF_CNT_BITS) | (uint32_t)(rootCount - 1));
+    BK(hipMalloc(out, W4_F4 * sizeof(float4)));
+    return hipMemsetAsync(*out, 0, W4_F4 * sizeof(float4), s);
+  }
+  // every wide node holds >= 2 binary nodes' worth of children: at most nNodes / 2 of them
+  const size_t maxW = (size_t)nNodes / 2 + 1;
+  int *frontA = nullptr, *frontB = nullptr, *cnt = nullptr, *scan = nullptr, *host = nullptr;
+  int4* kids = nullptr;
+  void* cub = nullptr;
+  size_t cubBytes = 0;
+  auto fin = [&](hipError_t r) {
+    (void)hipFree(frontA); (void)hipFree(frontB); (void)hipFree(cnt); (void)hipFree(scan); (void)hipFree(kids);
+    (void)hipFree(cub);
+    if (host) (void)hipHostFree(host);
+    if (r != hipSuccess) { (void)hipFree(*out); *out = nullptr; }
+    return r;
+  };
+  if ((e = hipMalloc(out, maxW * W4_F4 * sizeof(float4))) != hipSuccess || (e = hipMalloc(&frontA, maxW * sizeof(int))) ||
+      (e = hipMalloc(&frontB, maxW * sizeof(int))) || (e = hipMalloc(&cnt, (maxW + 1) * sizeof(int))) ||
+      (e = hipMalloc(&scan, (maxW + 1) * sizeof(int))) || (e = hipMalloc(&kids, maxW * sizeof(int4))) ||
+      (e = hipHostMalloc((void**)&host, sizeof(int))))
+    return fin(e);
+  if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, cubBytes, cnt, scan, (int)(maxW + 1), s)) ||
+      (e = hipMalloc(&cub, std::max<size_t>(cubBytes, 1))))
+    return fin(e);
+  const int zero = 0;
+  if ((e = hipMemcpyAsync(frontA, &zero, sizeof(int), hipMemcpyHostToDevice, s))) return fin(e);
+  int F = 1, base = 0, d = 0;
+  int* front = frontA;
+  int* next = frontB;
+  while (F > 0) {
+    hipLaunchKernelGGL(w4ExpandKernel, dim3(blocks(F + 1)), dim3(256), 0, s, nodes, front, F, leafSize, kids, cnt);
+    size_t cb = cubBytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(cub, cb, cnt, scan, F + 1, s))) return fin(e);
+    hipLaunchKernelGGL(w4EncodeKernel, dim3(blocks(F)), dim3(256), 0, s, nodes, kids, scan, F, base, leafSize, inflate,
+                       inflateRelAbs, *out, next);
+    if ((e = hipGetLastError()) || (e = hipMemcpyAsync(host, scan + F, sizeof(int), hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return fin(e);
+    base += F;
+    F = *host;
+    d++;
+    if ((size_t)base + F > maxW) return fin(hipErrorUnknown);  // cannot happen: every wide node splits a binary one
+    std::swap(front, next);
+  }
+  *nDev = base;
+  *depth = d;
+  *rootRef = 0;
+  return fin(hipSuccess);
 }
 
 void freeAccelBuild(AccelBuild& a) {

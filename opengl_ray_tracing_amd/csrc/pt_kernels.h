@@ -259,6 +259,10 @@ struct AccelBuild {
 hipError_t buildAccelDevice(const float4* geo, int nTri, int leafSize, float inflate, float inflateRelAbs,
                             AccelBuild& out, hipStream_t s);
 void freeAccelBuild(AccelBuild& a);
+// the build nodes collapsed to 4-wide records (SceneView::fbvh4, pt_runtime.cpp encodeWide4's
+// layout, ids and widening) on the device; *out allocated here (W4_F4 float4 per wide node)
+hipError_t collapseWide4Device(const BuildNode* nodes, int nNodes, int leafSize, float inflate, float inflateRelAbs,
+                               float4** out, int* rootRef, int* nDev, int* depth, hipStream_t s);
 
 // calculateHdrCache on the device (pt_envcache.hip); scratch: 2*w*h + 2*w + 1 floats
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);

@@ -875,7 +875,6 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   ctx->maxStack = h.ref.depth + 1;
   ctx->fastReady = false;
   ctx->fast4Ready = false;
-  std::vector<float> accelRef;  // the device-built tree in the reference encoding
   ctx->accelDevice = -1;
   ctx->accelMs = 0.0f;
   ctx->accelNodes = ctx->accelDepth = 0;
@@ -893,15 +892,17 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
       freeAccelBuild(ab);
       return PT_OK;
     }
-    // its nodes on the host, for the 4-wide collapse
-    std::vector<BuildNode> bn(ab.nNodes);
-    e = hipMemcpy(bn.data(), ab.nodes, bn.size() * sizeof(BuildNode), hipMemcpyDeviceToHost);
+    // the 4-wide collapse, on the device too (the large-scene regen kernel's and the megakernel's tree)
+    float4* w4 = nullptr;
+    e = collapseWide4Device(ab.nodes, ab.nNodes, PT_ACCEL_LEAF, 1e-5f, 3e-5f, &w4, &ctx->f4Root, &ctx->f4nDev,
+                            &ctx->f4Depth, ctx->stream);
     dfree(ab.nodes);
     if (e != hipSuccess) {
       freeAccelBuild(ab);
-      return fail(ctx, PT_E_HIP, std::string("device tree download: ") + hipGetErrorString(e));
+      return fail(ctx, PT_E_HIP, std::string("device 4-wide collapse: ") + hipGetErrorString(e));
     }
-    accelRef = refNodes(bn, PT_ACCEL_LEAF);
+    dfree(ctx->d_fbvh4);
+    ctx->d_fbvh4 = w4;
     dfree(ctx->d_fbvh);
     dfree(ctx->d_fpairs);
     dfree(ctx->d_fastTri);
@@ -926,19 +927,19 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
     ctx->accelNodes = h.accelNodes;
   }
   ctx->accelDepth = ctx->fDepth;
-  // the 4-wide collapse (the large-scene regen kernel's tree), widened like the binary records
-  {
-    const std::vector<float>& an = h.deviceBuild ? accelRef : h.accelRef;
+  // the host-built tree's 4-wide collapse (the device build collapsed on the device above)
+  if (!h.deviceBuild) {
+    const std::vector<float>& an = h.accelRef;
     const int nn = (int)(an.size() / 12);
     float scale = 0.0f;  // the scene's largest coordinate magnitude: the root box's
     for (int k = 6; k < 12 && nn > 1; k++) scale = std::max(scale, std::fabs(an[12 + k]));
     std::vector<float4> w4;
     encodeWide4(an.data(), nn, h.nTri, 1e-5f, 3e-5f * scale, w4, ctx->f4Root, ctx->f4nDev, ctx->f4Depth);
     if ((rc = upload(ctx, &ctx->d_fbvh4, w4))) return rc;
-    ctx->fast4Ready = true;
-    // a visit pushes up to three children: the traversal stack needs 3 entries per wide level
-    ctx->maxStack = std::max(ctx->maxStack, 3 * ctx->f4Depth + 2);
   }
+  ctx->fast4Ready = true;
+  // a visit pushes up to three children: the traversal stack needs 3 entries per wide level
+  ctx->maxStack = std::max(ctx->maxStack, 3 * ctx->f4Depth + 2);
   ctx->sceneVersion++;  // camera-ray bins are rebuilt for the new triangles
   ctx->maxStack = std::max(ctx->maxStack, ctx->fDepth + 1);
   ctx->fastReady = true;
