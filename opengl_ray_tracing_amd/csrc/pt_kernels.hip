@@ -291,20 +291,39 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
     }
   }
   if (p.binStart && b1 - b0 <= PT_BIN_CAP) {
+    // the bin's triangles staged in the wave's own (still empty) part of the LDS stack:
+    // every lane loads one float4 of one triangle, so the whole bin costs two memory round
+    // trips instead of one per triangle; the test loop then reads broadcast LDS records.
+    // Triangle t's 16 floats at wb + (t >> 2) * BLOCK + (t & 3) * 16, its index at row 8.
+    static_assert(PT_BIN_CAP <= 32 && LDS_STACK >= 9, "bin staging fits the wave's stack rows 0..8");
+    const int n = b1 - b0;
+    int* wb = st.lds - __lane_id();  // column 0 of this wave's stack columns
+    const int lane = __lane_id();
+    for (int t = lane >> 2; t < n; t += 16) {
+      const int i = p.binTris[b0 + t];
+      const float4 v = p.scene.geo[4 * (size_t)i + (lane & 3)];
+      *reinterpret_cast<float4*>(wb + (t >> 2) * BLOCK + (t & 3) * 16 + 4 * (lane & 3)) = v;
+      if ((lane & 3) == 0) wb[8 * BLOCK + t] = i;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float tbest = PT_INF;
     int best = -1;
     tie = false;
-    for (int k = b0; k < b1; k++) {
-      const int i = p.binTris[k];
-      const float4* g = p.scene.geo + 4 * (size_t)i;
+    for (int k = 0; k < n; k++) {
+      const float4* g = reinterpret_cast<const float4*>(wb + (k >> 2) * BLOCK + (k & 3) * 16);
       float tt;
       const bool h = valid && triTest(g[0], g[1], g[2], g[3], eye, dir, PT_INF, tt);
       if (h && tt == tbest) tie = true;
       if (h && tt < tbest) {
         tbest = tt;
-        best = i;
+        best = k;
       }
     }
+    if (best >= 0) best = wb[8 * BLOCK + best];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // every lane has read the staging before the stack is used
+    __builtin_amdgcn_wave_barrier();
     if (valid) C.rays++;
     tri = best;
     t = tbest;
