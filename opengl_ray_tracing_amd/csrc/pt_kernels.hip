@@ -294,8 +294,9 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
     // the bin's triangles staged in the wave's own (still empty) part of the LDS stack:
     // every lane loads one float4 of one triangle, so the whole bin costs two memory round
     // trips instead of one per triangle; the test loop then reads broadcast LDS records.
-    // Triangle t's 16 floats at wb + (t >> 2) * BLOCK + (t & 3) * 16, its index at row 8.
-    static_assert(PT_BIN_CAP <= 32 && LDS_STACK >= 9, "bin staging fits the wave's stack rows 0..8");
+    // Triangle t's 16 floats at wb + (t >> 2) * BLOCK + (t & 3) * 16, its index at row IDX.
+    constexpr int IDX = (PT_BIN_CAP + 3) / 4;
+    static_assert(PT_BIN_CAP <= 64 && IDX < LDS_STACK, "bin staging fits the wave's stack rows 0..IDX");
     const int n = b1 - b0;
     int* wb = st.lds - __lane_id();  // column 0 of this wave's stack columns
     const int lane = __lane_id();
@@ -303,7 +304,7 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
       const int i = p.binTris[b0 + t];
       const float4 v = p.scene.geo[4 * (size_t)i + (lane & 3)];
       *reinterpret_cast<float4*>(wb + (t >> 2) * BLOCK + (t & 3) * 16 + 4 * (lane & 3)) = v;
-      if ((lane & 3) == 0) wb[8 * BLOCK + t] = i;
+      if ((lane & 3) == 0) wb[IDX * BLOCK + t] = i;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -321,7 +322,7 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
         best = k;
       }
     }
-    if (best >= 0) best = wb[8 * BLOCK + best];
+    if (best >= 0) best = wb[IDX * BLOCK + best];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // every lane has read the staging before the stack is used
     __builtin_amdgcn_wave_barrier();
     if (valid) C.rays++;
