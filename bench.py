@@ -129,8 +129,9 @@ def main():
         from opengl_ray_tracing_amd.distributed import SampleReduce
         combine = SampleReduce(r, rank, n, f"cuda:{local}")
 
-    def step(frame):
-        r.render_frame(eye, rot, frame, sync=False)
+    def step(frame, cam=None):
+        e, c = cam if cam is not None else (eye, rot)
+        r.render_frame(e, c, frame, sync=False)
         if gather is not None:
             gather()
 
@@ -157,14 +158,17 @@ def main():
     sync_all()
     t1 = time.perf_counter()
     st = r.stats()
-    # interactive cost after a camera reset (the reference zeroes frameCounter on every mouse
-    # move, OpenglRayTracing/main.cpp:611-634): frames 0..PROBE_FRAMES-1 of a restarted running
-    # mean, including the renderer's policy probe, timed like the steps
+    # interactive cost after a camera move (the reference's mouse() rotates the camera and zeroes
+    # frameCounter, OpenglRayTracing/main.cpp:611-634): frames 0..PROBE_FRAMES-1 of a restarted
+    # running mean from a camera rotated by one degree, timed like the steps -- the camera-ray
+    # bins are rebuilt and the per-tile split state starts over; the tree / split policies
+    # probed after the upload are kept (pt_runtime.cpp probePolicy)
     reset_ms = None
     if not args.no_reset:
+        moved = orbit_camera(cfg.camera[0] + 1.0, *cfg.camera[1:])
         t2 = time.perf_counter()
         for f in range(PROBE_FRAMES):
-            step(f)
+            step(f, moved)
         sync_all()
         reset_ms = 1e3 * (time.perf_counter() - t2) / PROBE_FRAMES
     combined_finite = None

@@ -133,6 +133,7 @@ struct pt_ctx {
   long long probeLast[3] = {-1, -1, -1};  // launch number of each slot's last timed frame
   int probeGen = 0;
   int treeDecided = -1, splitDecided = -1;  // -1 probing, 0 off, 1 on
+  unsigned policyKey = 0, probedKey = ~0u;  // bumped by every scene / env upload; the key the decisions were made for
   int orderCap = 0;        // work items per band in d_order
   bool orderValid[PIPE] = {};
   size_t ovfInts = 0;
@@ -860,6 +861,7 @@ static int syncStreams(pt_ctx* ctx);
 
 static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   if (int rc = syncStreams(ctx)) return rc;  // no frame in flight reads the buffers replaced here
+  ctx->policyKey++;  // the tree / split policies are measured again at the next restart
   CK(hipSetDevice(ctx->cfg.device_id));
   int rc;
   if ((rc = upload(ctx, &ctx->d_pairs, h.pairs)) || (rc = upload(ctx, &ctx->d_geo, h.geo)) ||
@@ -1057,6 +1059,7 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
     (void)hipFree(full);
     if (rc) return rc;
   }
+  ctx->policyKey++;
   ctx->hdrW = w;
   ctx->hdrH = h;
   return PT_OK;
@@ -1355,9 +1358,13 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
 // waits for frame 4 (frame 5 is already queued, so the GPU never drains) and
 // keeps the faster tree; frames 6-10 split (the per-tile split state
 // converges), 11-12 are timed, and at frame 14 -- waiting for frame 12 with 13
-// queued -- the faster split policy is kept until the next restart. No frame
-// waits for its own predecessor. Sets *useFast; returns the split percentage
-// for this frame's reorder (0 = off).
+// queued -- the faster split policy is kept. No frame waits for its own
+// predecessor. The decisions are kept across later restarts until the scene or
+// the env is uploaded again (a camera move changes neither tree's merit nor,
+// measurably, the split policy's), so only the first restart after an upload
+// pays for the probe's slower trial frames; every restart still clears the
+// per-tile split state and cost estimates. Sets *useFast; returns the split
+// percentage for this frame's reorder (0 = off).
 static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast) {
   *useFast = fastAllowed;
   ctx->tagSlot = -1;
@@ -1371,7 +1378,9 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
       ctx->probeMs[k] = 0.0;
       ctx->probeLast[k] = -1;
     }
-    ctx->treeDecided = ctx->splitDecided = -1;
+    const bool keep = ctx->treeDecided >= 0 && ctx->splitDecided >= 0 && ctx->probedKey == ctx->policyKey;
+    if (!keep) ctx->treeDecided = ctx->splitDecided = -1;
+    ctx->probedKey = ctx->policyKey;
     // split state and cost estimates start over (the camera or scene changed), in
     // every slot's stream order (after its last reorder, before its next frame)
     if (ctx->d_cost)
