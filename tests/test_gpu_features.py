@@ -318,3 +318,31 @@ def test_device_group_equals_one_device(devices):
     assert st.rays == ref_st.rays
     with pytest.raises(_native.PtError):  # RCCL needs distinct devices
         Renderer(w, h, "lambert", devices=devices, gather="rccl")
+
+
+@pytest.mark.parametrize("name", ["c2", "c4"])
+def test_camera_restart_keeps_policies_and_restarts_the_mean(name):
+    """A camera move restarts the running mean (frameCounter 0, OpenglRayTracing/main.cpp:611-634):
+    the next frames equal a fresh context's frames of the moved camera bit for bit, while the
+    tree / split policies probed after the upload are kept (pt_runtime.cpp probePolicy)."""
+    cfg, tris, nodes, hdr = scenes.build_config(name)
+    w, h = 480, 270
+    a = orbit_camera(*cfg.camera)
+    b = orbit_camera(cfg.camera[0] + 7.0, cfg.camera[1] + 3.0, cfg.camera[2])
+    with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce) as r:
+        r.upload_scene(tris, nodes)
+        r.upload_env(hdr)
+        for f in range(20):  # past the 14-frame policy probe
+            r.render_frame(*a, f)
+        tree = r.stats().runtime_tree
+        for f in range(3):
+            r.render_frame(*b, f)
+        moved = r.accum()
+        assert r.stats().runtime_tree == tree
+    with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce) as r:
+        r.upload_scene(tris, nodes)
+        r.upload_env(hdr)
+        for f in range(3):
+            r.render_frame(*b, f)
+        fresh = r.accum()
+    assert np.array_equal(moved, fresh)
