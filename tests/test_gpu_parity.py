@@ -238,6 +238,17 @@ def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
     o, _ = render_oracle(cfg, tris, nodes, hdr, px, frames=2, max_bounce=mb, w=w, h=h)
     parity.assert_parity(g[px[:, 1], px[:, 0]], o[px[:, 1], px[:, 0]], "wide/mis")
     assert np.all(g[..., 3] == 1.0)
+    # the uniform Disney integrator (D:443-481) takes the same large-scene kernel; Lambert keeps
+    # the megakernel (its paths are short)
+    d, sd = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator="disney", max_bounce=mb, w=w, h=h)
+    dm, sdm = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator="disney", max_bounce=mb, w=w, h=h,
+                         flags=FLAG_MEGAKERNEL)
+    assert sd.regen == 1 and sdm.regen == 0
+    assert np.array_equal(d, dm) and sd.rays == sdm.rays
+    od, _ = render_oracle(cfg, tris, nodes, hdr, px, frames=2, integrator="disney", max_bounce=mb, w=w, h=h)
+    parity.assert_parity(d[px[:, 1], px[:, 0]], od[px[:, 1], px[:, 0]], "wide/disney")
+    _, sl = render_gpu(cfg, tris, nodes, hdr, frames=1, integrator="lambert", max_bounce=mb, w=w, h=h)
+    assert sl.regen == 0
 
 
 @pytest.mark.parametrize("name,tile", [("c4", (0, 1)), ("c2", (1, 3))])

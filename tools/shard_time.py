@@ -40,11 +40,14 @@ def main():
             t0 = time.perf_counter()
             for f in range(24, 24 + K):
                 r.render_frame(eye, rot, f, sync=False)
+            t_sub = time.perf_counter()
             r.synchronize()
             ms = 1e3 * (time.perf_counter() - t0) / K
+            submit_ms = 1e3 * (t_sub - t0) / K  # host time per pt_render_frame_async call
             st = r.stats()
         print(json.dumps({"variant": os.environ.get("PT_VARIANT", "base"), "config": cfg_name, "world": n, "rank0_ms_per_frame": round(ms, 4),
                           "kernel_ms_avg": round(st.kernel_ms_total / max(st.launches, 1), 4),
+                          "host_submit_ms": round(submit_ms, 4),
                           "rays_per_frame": st.rays // max(st.launches, 1)}), flush=True)
 
 
