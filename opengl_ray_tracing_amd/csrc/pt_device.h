@@ -206,14 +206,13 @@ __device__ __forceinline__ V3 hdrColor(const Env& e, V3 L) {
   float4 c = texNearest(e.hdr, e.w, e.h, u, w);
   return v3(c.x, c.y, c.z);
 }
-// SampleHdr IS:573-585
-__device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
-  float x = 0.0f, y = 0.0f;
-  if (e.cache) {
-    float2 c = texNearest(e.cache, e.w, e.h, xi1, xi2);
-    x = c.x;
-    y = c.y;
-  }
+// SampleHdr IS:573-585, in two parts: the cache texel of (xi1, xi2) and the
+// direction it encodes (split so a caller can issue the fetch early)
+__device__ __forceinline__ float2 hdrCacheTexel(const Env& e, float xi1, float xi2) {
+  return e.cache ? texNearest(e.cache, e.w, e.h, xi1, xi2) : make_float2(0.0f, 0.0f);
+}
+__device__ __forceinline__ V3 hdrDirFromCache(float2 c) {
+  float x = c.x, y = c.y;
   y = 1.0f - y;
   float phi = 2.0f * PT_PI * (x - 0.5f);
   float theta = PT_PI * (y - 0.5f);
@@ -221,6 +220,9 @@ __device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
   ptm_sincosf(theta, &st, &ct);
   ptm_sincosf(phi, &sp, &cp);
   return v3(ct * cp, st, ct * sp);
+}
+__device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
+  return hdrDirFromCache(hdrCacheTexel(e, xi1, xi2));
 }
 // hdrPdf IS:655-666 (sin of the elevation: reference quirk kept)
 __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
@@ -235,16 +237,25 @@ __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
 
 // hdrColor(L) and hdrPdf(L) of the same direction (every MIS use pairs them):
 // one toSphericalCoord, the same operations and results as the two calls.
-__device__ __forceinline__ void hdrColorPdf(const Env& e, V3 L, V3& color, float& pdf) {
-  float u, w;
+// Split in two like sampleHdrDir: the texel of L (and the elevation coordinate
+// w its pdf needs), then color and pdf from them.
+__device__ __forceinline__ float4 hdrTexelOf(const Env& e, V3 L, float& w) {
+  float u;
   toSpherical(normalize(L), u, w);
-  const float4 c = e.hdr ? texNearest(e.hdr, e.w, e.h, u, w) : make_float4(0, 0, 0, 0);
+  return e.hdr ? texNearest(e.hdr, e.w, e.h, u, w) : make_float4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void hdrColorPdfOf(const Env& e, float4 c, float w, V3& color, float& pdf) {
   color = v3(c.x, c.y, c.z);
   const float p = c.w;  // the cache pdf of the same texel
   const float theta = PT_PI * (0.5f - w);
   const float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
   const float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
   pdf = p * p_convert;
+}
+__device__ __forceinline__ void hdrColorPdf(const Env& e, V3 L, V3& color, float& pdf) {
+  float w;
+  const float4 c = hdrTexelOf(e, L, w);
+  hdrColorPdfOf(e, c, w, color, pdf);
 }
 
 // ------------------------------------------------------------ BRDF IS:386-711

@@ -85,6 +85,9 @@ constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
 // 1 = without (c3 0.257, c2 0.380), 0 = the binary runtime tree
 #define PT_WIDE4 2
 #endif
+#ifndef PT_LIGHT_PREFETCH
+#define PT_LIGHT_PREFETCH 0  // MIS: fetch the next bounce's env light sample before this bounce's walks
+#endif
 #ifndef PT_FUSED_SLABS
 #define PT_FUSED_SLABS 1  // the runtime tree's slab tests as packed FMAs (pt_trace.h visitNodeF)
 #endif

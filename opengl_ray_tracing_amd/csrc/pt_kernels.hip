@@ -164,20 +164,48 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
   const uint32_t gi = grayCode(frameCounter + 1u);  // frameCounter = the sample index here
   float cpu, cpv;
   cranleyPattersonShift(px, py, cpu, cpv);
+#if PT_LIGHT_PREFETCH
+  // The light sample of a bounce depends only on the RNG state at its start
+  // (r1, r2 -> cache texel -> direction -> env texel), which is known one
+  // bounce early: bounce b + 1's cache texel is fetched before bounce b's
+  // shadow walk and its env texel before the closest-hit walk, so neither
+  // dependent Infinity-Cache fetch sits on the path's chain. Same operations
+  // on the same values; the RNG is advanced where the reference draws.
+  V3 LdirN;
+  float4 texN;
+  float wN;
+  {
+    uint32_t s = seed;
+    const float a = randf(s);
+    const float b = randf(s);
+    LdirN = hdrDirFromCache(hdrCacheTexel(env, a, b));
+    texN = hdrTexelOf(env, LdirN, wN);
+  }
+#endif
   for (int bounce = 0; bounce < maxBounce; bounce++) {
     const V3 V = -hit.viewDir;
     const V3 N = hit.N;
     // (1) light sample IS:772-789
     const float r1 = randf(seed);
     const float r2 = randf(seed);
+#if PT_LIGHT_PREFETCH
+    (void)r1;
+    (void)r2;
+    const V3 Ldir = LdirN;
+#else
     const V3 Ldir = sampleHdrDir(env, r1, r2);
+#endif
     if (count) C.texels++;
     const bool tryLight = dot(N, Ldir) > 0.0f;
     V3 lightC = v3(0, 0, 0);
     if (tryLight) {
       V3 color;
       float pdf_light;
+#if PT_LIGHT_PREFETCH
+      hdrColorPdfOf(env, texN, wN, color, pdf_light);
+#else
       hdrColorPdf(env, Ldir, color, pdf_light);
+#endif
       V3 f_r = brdfIso(V, N, Ldir, hit.m);
       float pdf_brdf = brdfPdf(V, N, Ldir, hit.m);
       float mis_weight = misWeight(pdf_light, pdf_brdf);
@@ -193,11 +221,26 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
     const float NdotL = dot(N, L);
     const V3 f_r = brdfIso(V, N, L, hit.m);
     const float pdf_brdf = brdfPdf(V, N, L, hit.m);
+#if PT_LIGHT_PREFETCH
+    float2 cacheN = make_float2(0.0f, 0.0f);
+    if (bounce + 1 < maxBounce) {
+      uint32_t s = seed;
+      const float a = randf(s);
+      const float b = randf(s);
+      cacheN = hdrCacheTexel(env, a, b);
+    }
+#endif
     if (tryLight && !tr.occluded(hit.P, Ldir)) {
       Lo = Lo + lightC;
       if (count) C.texels += 2;
     }
     if (NdotL <= 0.0f) break;
+#if PT_LIGHT_PREFETCH
+    if (bounce + 1 < maxBounce) {
+      LdirN = hdrDirFromCache(cacheN);
+      texN = hdrTexelOf(env, LdirN, wN);
+    }
+#endif
     Hit nh;
     bool isHit = tr.closest(hit.P, L, nh);
     if (pdf_brdf <= 0.0f) break;
