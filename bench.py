@@ -48,7 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # at the 2.4 GHz maximum clock (MI355X_MICROARCH.md "Wave scheduling"): 1228.8 G wave-instructions/s
 VALU_PEAK_GINST = 1024 * 2.4 / 2 * 1e9 / 1e9
 METRIC = "Mrays/sec + ms/frame (1 spp, 1080p) at 1/2/4/8 MI355X; CPU-ref spp-matched PSNR"
-PROBE_FRAMES = 14  # frames after a restart during which the renderer measures its tree and split policies
+PROBE_FRAMES = 20  # frames after a restart during which the renderer measures its tree and split policies
 
 
 def parse():

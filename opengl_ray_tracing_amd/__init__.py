@@ -6,12 +6,12 @@ C ABI of libpt.so. There is no CPU fallback in this package.
 """
 from .scene import (Material, Scene, calculate_hdr_cache, decode_hdr, get_transform_matrix, load_hdr,
                     orbit_camera, read_pfm, write_pfm, write_png)
-from .renderer import (FLAG_CLOSEST_SHADOW, FLAG_COUNT_FETCHES, FLAG_NO_CULL, FLAG_NO_TILE_ORDER, FLAG_REFERENCE_TREE, FLAG_SERIAL_FRAMES, FLAG_NO_BINS, FLAG_HOST_ACCEL, FLAG_MEGAKERNEL, FLAG_REGEN, FLAG_WAVEFRONT, INTEGRATORS,
+from .renderer import (FLAG_CLOSEST_SHADOW, FLAG_COUNT_FETCHES, FLAG_NO_CULL, FLAG_NO_TILE_ORDER, FLAG_REFERENCE_TREE, FLAG_SERIAL_FRAMES, FLAG_NO_BINS, FLAG_HOST_ACCEL, FLAG_MEGAKERNEL, FLAG_PRIMARY_PASS, FLAG_REGEN, FLAG_WAVEFRONT, INTEGRATORS,
                        FrameStats, Renderer, device_count)
 
 __all__ = [
     "Material", "Scene", "calculate_hdr_cache", "decode_hdr", "get_transform_matrix", "load_hdr", "orbit_camera",
     "read_pfm", "write_pfm", "write_png",
     "Renderer", "FrameStats", "device_count", "INTEGRATORS", "FLAG_NO_CULL", "FLAG_CLOSEST_SHADOW",
-    "FLAG_COUNT_FETCHES", "FLAG_HOST_ACCEL", "FLAG_MEGAKERNEL", "FLAG_NO_TILE_ORDER", "FLAG_REFERENCE_TREE", "FLAG_REGEN", "FLAG_WAVEFRONT",
+    "FLAG_COUNT_FETCHES", "FLAG_HOST_ACCEL", "FLAG_MEGAKERNEL", "FLAG_PRIMARY_PASS", "FLAG_NO_TILE_ORDER", "FLAG_REFERENCE_TREE", "FLAG_REGEN", "FLAG_WAVEFRONT",
 ]

@@ -85,6 +85,9 @@ constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
 // 1 = without (c3 0.257, c2 0.380), 0 = the binary runtime tree
 #define PT_WIDE4 2
 #endif
+#ifndef PT_CLAIM_AHEAD
+#define PT_CLAIM_AHEAD 0  // megakernel: claim the next tile when a tile starts (TileCursor::claimAhead)
+#endif
 #ifndef PT_LIGHT_PREFETCH
 #define PT_LIGHT_PREFETCH 0  // MIS: fetch the next bounce's env light sample before this bounce's walks
 #endif
@@ -171,7 +174,13 @@ struct RenderParams {
   const int* binStart;
   const int* binTris;
   int binTilesX, binTilesY;
-  int* queue;           // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
+  // camera-ray pass (primaryKernel): per pixel (py * width + px) the camera ray's result,
+  // {tri, t bits}: tri >= 0 a hit, PRIM_MISS (finished: sky colour written), PRIM_RETRACE
+  // (a tie or an unreachable winner: the megakernel traces it in the reference order),
+  // PRIM_TILE (the tile's bin is over PT_BIN_CAP: the megakernel traces the tile's
+  // packet); null = the megakernel traces its camera rays itself
+  int2* primHit;
+  int* queue;          // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
   int perQueue;         // items per queue
   int numItems;         // 8x8 wave tiles owned by this rank
   int shardSize;        // shard tile edge (multiple of 8)
@@ -282,6 +291,9 @@ constexpr int REORDER_MAX = 4096;  // most groups per band the one-block LDS sor
 hipError_t launchReorder(int* cost, int* costMax, int* splitLg, int* ema, int* order, int perQueue, int orderCap,
                          int numItems, int group, int numWaves, int splitPct, hipStream_t s);
 hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, bool wide, int* nb);
+// the camera-ray pass: one wave per 8x8 tile of the rank's tiles, results in p.primHit
+constexpr int PRIM_MISS = -1, PRIM_RETRACE = -2, PRIM_TILE = -3;
+hipError_t launchPrimary(const RenderParams& p, hipStream_t s);
 // the path-regeneration kernel (pt_regen.hip); wide: the large-scene variant (WIDE_REGEN_WAVES)
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool wide = false);
 hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb);

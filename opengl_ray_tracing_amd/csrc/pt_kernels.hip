@@ -403,6 +403,82 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
   return tri;
 }
 
+// Camera-ray pass: the bin path of primaryPacket for every 8x8 tile of the
+// rank, one wave per tile, before the megakernel. Inside the persistent
+// megakernel (3 waves/SIMD) a tile's camera rays are a chain of dependent
+// round trips (claim, bin, triangles, refReachable, env) that the few resident
+// waves cannot hide; here a launch of one short wave per tile keeps up to 8
+// waves per SIMD in flight and claims nothing. Sky pixels are finished here;
+// every other pixel's result goes to primHit for the megakernel.
+__global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
+  __shared__ float4 s_tri[PT_BIN_CAP * 4];
+  __shared__ int s_idx[PT_BIN_CAP];
+  const int w = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int sub = p.shardSize >> 3;
+  const int j = w / p.shardTiles, s = w - j * p.shardTiles;
+  const int g = j * p.world + p.rank;
+  const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
+  const int px = gx * p.shardSize + (s % sub) * 8 + (lane & 7);
+  const int py = gy * p.shardSize + (s / sub) * 8 + (lane >> 3);
+  const bool valid = px < p.width && py < p.height;
+  const int tx = (gx * p.shardSize + (s % sub) * 8) >> 3, ty = (gy * p.shardSize + (s / sub) * 8) >> 3;
+  int b0 = 0, b1 = 0;  // a tile wholly outside the image has no bin (and no valid lane)
+  if (tx < p.binTilesX && ty < p.binTilesY) {
+    b0 = p.binStart[ty * p.binTilesX + tx];
+    b1 = p.binStart[ty * p.binTilesX + tx + 1];
+  }
+  const int n = b1 - b0;
+  int2* out = p.primHit + (size_t)py * p.width + px;
+  if (n > PT_BIN_CAP) {  // the megakernel traces this tile's camera rays as a packet
+    if (valid) *out = make_int2(PRIM_TILE, 0);
+    return;
+  }
+  for (int t = lane >> 2; t < n; t += 16) {  // one float4 of one triangle per lane
+    const int i = p.binTris[b0 + t];
+    s_tri[4 * t + (lane & 3)] = p.scene.geo[4 * (size_t)i + (lane & 3)];
+    if ((lane & 3) == 0) s_idx[t] = i;
+  }
+  __syncthreads();
+  uint32_t seed;
+  const V3 dir = cameraRay(p, valid ? px : 0, valid ? py : 0, seed);
+  const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+  float tbest = PT_INF;
+  int best = -1;
+  bool tie = false;
+  for (int k = 0; k < n; k++) {
+    float tt;
+    const bool h = valid && triTest(s_tri[4 * k], s_tri[4 * k + 1], s_tri[4 * k + 2], s_tri[4 * k + 3], eye, dir,
+                                    PT_INF, tt);
+    if (h && tt == tbest) tie = true;
+    if (h && tt < tbest) {
+      tbest = tt;
+      best = k;
+    }
+  }
+  uint32_t rays = 0;
+  if (valid) {
+    int res = best >= 0 ? s_idx[best] : PRIM_MISS;
+    if (tie || (res >= 0 && !refReachable(p.scene, res, eye, dir, tbest))) {
+      res = PRIM_RETRACE;  // counted by the megakernel's retrace
+    } else {
+      rays = 1;
+      if (res == PRIM_MISS) {
+        Counters C = {0, 0, 0, 0, 0};
+        accumulate(p, px, py, sampleHdr(p.env, dir), C, false);
+      }
+    }
+    *out = make_int2(res, __float_as_int(tbest));
+  }
+  addRays(p.rayShards, rays);
+}
+
+hipError_t launchPrimary(const RenderParams& p, hipStream_t s) {
+  if (!p.primHit || !p.binStart || p.numItems <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(primaryKernel, dim3(p.numItems), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+
 // the rest of the path of a pixel whose camera ray hit triangle tri at t
 template <int INTEG, bool CULL, bool COUNT>
 __device__ __forceinline__ void finishPixel(const RenderParams& p, int px, int py, int tri, float t, Stack& st,
@@ -752,9 +828,11 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   // queue and running them 64 at a time keeps every lane busy, but it mixes
   // tiles: 64-path batches made c2 0.77 ms instead of 0.55, 32-path batches
   // 0.59 -- the coherence of one tile's rays is worth more than full lanes.)
-  while (true) {
-    const int item = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
-    if (item < 0) break;
+  int item = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+  while (item >= 0) {
+#if PT_CLAIM_AHEAD
+    cur.claimAhead(p.queue, home);
+#endif
     const int w = itemTile(item);
     const long long t0 = COUNT ? 0 : clock64();
 #if PT_WAVE_TRACE
@@ -770,7 +848,21 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     const int px = gx * p.shardSize + (s % sub) * 8 + (k & 7);
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
     const bool valid = lane < nLanes && px < p.width && py < p.height;
-    if (!COUNT && (p.packets || p.binStart)) {
+    if (!COUNT && p.primHit) {  // camera rays already traced by primaryKernel
+      const int2 h = valid ? p.primHit[(size_t)py * p.width + px] : make_int2(PRIM_MISS, 0);
+      int tri = h.x;
+      float t = __int_as_float(h.y);
+      if (__ballot(valid && tri == PRIM_TILE)) {  // wave-uniform: the whole tile
+        tri = primaryPacket<CULL>(p, px, py, valid, st, C, top, pstack, t);
+      } else if (valid && tri == PRIM_RETRACE) {  // in the reference order, as primaryPacket does
+        uint32_t seed;
+        const V3 dir = cameraRay(p, px, py, seed);
+        const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+        tri = traceRay<false, CULL, false, Stack>(p.scene, eye, dir, t, st, C);
+        if (tri < 0) accumulate(p, px, py, sampleHdr(p.env, dir), C, false);
+      }
+      if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);
+    } else if (!COUNT && (p.packets || p.binStart)) {
       float t;
       const int tri = primaryPacket<CULL>(p, px, py, valid, st, C, top, pstack, t);
       if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);
@@ -799,6 +891,11 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
       wLongest = tEnd - tw0;
       wLongestAt = (unsigned long long)__shfl(px, 0, 64) << 16 | (unsigned long long)__shfl(py, 0, 64);
     }
+#endif
+#if PT_CLAIM_AHEAD
+    item = cur.nextAhead(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+#else
+    item = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
 #endif
   }
 #if PT_WAVE_TRACE

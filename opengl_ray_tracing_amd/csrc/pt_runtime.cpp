@@ -125,14 +125,15 @@ struct pt_ctx {
   hipEvent_t mixDone[PIPE] = {};            // slot's last running-mean update
   hipEvent_t userMark = nullptr;            // the caller's stream at the last frame's call
   float4* d_col[PIPE] = {};                 // per-slot sample colours
+  int2* d_prim[PIPE] = {};                  // per-slot camera-ray results (primaryKernel)
   int lastSlot = -1;                        // slot of the last pipelined frame
   bool mixPending = false;                  // a pipelined frame's update may still be running
   unsigned long long frameNo = 0;           // pipelined frames issued
-  int probeN[3] = {0, 0, 0};           // timed frames: runtime tree, uploaded tree (both unsplit), split
-  double probeMs[3] = {0.0, 0.0, 0.0};
-  long long probeLast[3] = {-1, -1, -1};  // launch number of each slot's last timed frame
+  int probeN[4] = {0, 0, 0, 0};        // timed frames: runtime tree, uploaded tree (both unsplit), split, unordered
+  double probeMs[4] = {0.0, 0.0, 0.0, 0.0};
+  long long probeLast[4] = {-1, -1, -1, -1};  // launch number of each slot's last timed frame
   int probeGen = 0;
-  int treeDecided = -1, splitDecided = -1;  // -1 probing, 0 off, 1 on
+  int treeDecided = -1, splitDecided = -1, orderDecided = -1;  // -1 probing, 0 off, 1 on
   unsigned policyKey = 0, probedKey = ~0u;  // bumped by every scene / env upload; the key the decisions were made for
   int orderCap = 0;        // work items per band in d_order
   bool orderValid[PIPE] = {};
@@ -370,6 +371,7 @@ void pt_destroy(pt_ctx* ctx) {
   for (int k = 0; k < PIPE; k++) {
     if (ctx->slotStream[k]) (void)hipStreamSynchronize(ctx->slotStream[k]);
     dfree(ctx->d_col[k]);
+    dfree(ctx->d_prim[k]);
     if (ctx->mixDone[k]) (void)hipEventDestroy(ctx->mixDone[k]);
     if (ctx->slotStream[k]) (void)hipStreamDestroy(ctx->slotStream[k]);
   }
@@ -1351,35 +1353,44 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
 //  * tile splitting (reorderKernel) pays off when the SIMDs have issue slots to
 //    spare (the MIS integrator, latency-bound) and costs when they do not (the
 //    Lambert megakernel is VALU-bound: a split item's idle lanes still take
-//    issue cycles).
+//    issue cycles);
+//  * longest-first tile order itself (per-tile cost atomics, the order lookup
+//    of every claim, the reorder kernel) pays off when tiles differ widely in
+//    cost (c4: 8-bounce MIS around the teapot, 0.59 -> 0.47 ms) and costs when
+//    they do not (c2: 0.347 ms in band order vs 0.372 ordered).
 // After a restart of the running mean (frameCounter 0, as on every camera move
 // in the reference): frames 1-2 run the runtime's tree and 3-4 the uploaded
 // one, unsplit; frame 5 runs the runtime's tree while the host, at frame 6,
 // waits for frame 4 (frame 5 is already queued, so the GPU never drains) and
 // keeps the faster tree; frames 6-10 split (the per-tile split state
 // converges), 11-12 are timed, and at frame 14 -- waiting for frame 12 with 13
-// queued -- the faster split policy is kept. No frame waits for its own
-// predecessor. The decisions are kept across later restarts until the scene or
+// queued -- the faster split policy is kept; frames 15-16 run in band order
+// (no cost recording, no reorder) and at frame 19, waiting for frame 16, the
+// order is kept only if it was faster. No frame waits for its own predecessor. The decisions are kept across later restarts until the scene or
 // the env is uploaded again (a camera move changes neither tree's merit nor,
 // measurably, the split policy's), so only the first restart after an upload
 // pays for the probe's slower trial frames; every restart still clears the
-// per-tile split state and cost estimates. Sets *useFast; returns the split
-// percentage for this frame's reorder (0 = off).
-static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast) {
+// per-tile split state and cost estimates. Sets *useFast and *noOrder (this
+// frame in band order); returns the split percentage for this frame's reorder
+// (0 = off).
+static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast,
+                       bool* noOrder) {
   *useFast = fastAllowed;
+  *noOrder = false;
   ctx->tagSlot = -1;
   if (!ordered) return 0;
   if (!PT_SPLIT_AUTO) return PT_SPLIT_PCT;
   if (frameCounter == 0) {
     ctx->probeGen++;
     ctx->probeFrame = 0;
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < 4; k++) {
       ctx->probeN[k] = 0;
       ctx->probeMs[k] = 0.0;
       ctx->probeLast[k] = -1;
     }
-    const bool keep = ctx->treeDecided >= 0 && ctx->splitDecided >= 0 && ctx->probedKey == ctx->policyKey;
-    if (!keep) ctx->treeDecided = ctx->splitDecided = -1;
+    const bool keep = ctx->treeDecided >= 0 && ctx->splitDecided >= 0 && ctx->orderDecided >= 0 &&
+                      ctx->probedKey == ctx->policyKey;
+    if (!keep) ctx->treeDecided = ctx->splitDecided = ctx->orderDecided = -1;
     ctx->probedKey = ctx->policyKey;
     // split state and cost estimates start over (the camera or scene changed), in
     // every slot's stream order (after its last reorder, before its next frame)
@@ -1398,6 +1409,15 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
     foldUpTo(ctx, ctx->probeLast[2]);
     ctx->splitDecided = PT_SPLIT_PCT > 0 && avg(2) < avg(ctx->treeDecided ? 0 : 1) ? 1 : 0;
   }
+  if (f == 19 && ctx->orderDecided < 0) {
+    foldUpTo(ctx, ctx->probeLast[3]);
+    ctx->orderDecided = avg(3) < avg(ctx->splitDecided ? 2 : ctx->treeDecided ? 0 : 1) ? 0 : 1;
+  }
+  // this frame's tile order
+  if (ctx->orderDecided == 0 || (ctx->orderDecided < 0 && (f == 15 || f == 16))) {
+    *noOrder = true;
+    if (ctx->orderDecided < 0) ctx->tagSlot = 3;
+  }
   // this frame's tree, and the probe slot its time goes to
   if (ctx->treeDecided >= 0) {
     *useFast = fastAllowed && ctx->treeDecided;
@@ -1408,7 +1428,7 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
   // this frame's split policy (for the next frame's items)
   if (ctx->splitDecided >= 0) return ctx->splitDecided ? PT_SPLIT_PCT : 0;
   if (f == 11 || f == 12) ctx->tagSlot = 2;
-  return f >= 6 ? PT_SPLIT_PCT : 0;
+  return f >= 6 && f < 15 ? PT_SPLIT_PCT : 0;
 }
 
 static PackParams packParams(const pt_ctx* ctx, int rank, int world);
@@ -1528,9 +1548,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   int* order = ordered ? ctx->d_order + (size_t)slot * orderInts : nullptr;
   // the tree (the runtime's own, checked against the uploaded one, unless asked
   // not to) and the split policy: probePolicy
-  bool useFast = false;
+  bool useFast = false, noOrder = false;
   const int splitPct = probePolicy(ctx, frameCounter, ordered,
-                                   !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast);
+                                   !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast,
+                                   &noOrder);
   // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
   if (regen && wide && ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE)) useFast = true;
   p.scene.fast = useFast ? 1 : 0;
@@ -1555,14 +1576,23 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     p.binTris = ctx->bins.binTris;
     p.binTilesX = ctx->bins.tilesX;
     p.binTilesY = ctx->bins.tilesY;
+    // the camera-ray pass (primaryKernel) ahead of the megakernel, on request
+    if (c.flags & PT_FLAG_PRIMARY_PASS) {
+      if (!ctx->d_prim[slot]) CK(hipMalloc(&ctx->d_prim[slot], npix * sizeof(int2)));
+      p.primHit = ctx->d_prim[slot];
+    }
   }
-  p.tileOrder = ordered && ctx->orderValid[slot] ? order : nullptr;
+  // a frame in band order (probePolicy) records no costs and launches no reorder; the
+  // slot's last order list stays valid for its next ordered frame (any list covers every tile)
+  const bool orderedNow = ordered && !noOrder;
+  p.tileOrder = orderedNow && ctx->orderValid[slot] ? order : nullptr;
   p.orderCap = orderCap;
-  p.tileCost = cost;
-  p.tileCostMax = ordered ? cost + ctx->numItems : nullptr;
-  // While the policy probe times frames (PT_SPLIT_AUTO, 14 frames after a restart)
+  p.tileCost = orderedNow ? cost : nullptr;
+  p.tileCostMax = orderedNow ? cost + ctx->numItems : nullptr;
+  // While the policy probe times frames (PT_SPLIT_AUTO, 20 frames after a restart)
   // a pipelined frame still starts only after the previous one has ended.
-  const bool probing = ordered && PT_SPLIT_AUTO && (ctx->treeDecided < 0 || ctx->splitDecided < 0);
+  const bool probing = ordered && PT_SPLIT_AUTO &&
+                       (ctx->treeDecided < 0 || ctx->splitDecided < 0 || ctx->orderDecided < 0);
   if (piped && probing && ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
   int erc = launchEvents(ctx, &evb, &eve);
   if (erc) return erc;
@@ -1579,6 +1609,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.waveTrace = dTrace;
 #endif
   CK(hipEventRecord(evb, S));
+  if (p.primHit) CK(launchPrimary(p, S));
   if (regen) CK(launchRegen(p, c.integrator, grid, S, cull, wide));
   else CK(launchRender(p, c.integrator, grid, S, cull, count, wide));
 #if PT_WAVE_TRACE
@@ -1595,12 +1626,14 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     }
   }
 #endif
-  CK(hipEventRecord(eve, S));  // kernel_ms: the frame kernel alone (the reorder below is in the frame's wall time)
-  if (ordered) {
+  if (orderedNow) {
     CK(launchReorder(cost, cost + ctx->numItems, cost + 2 * (size_t)ctx->numItems, cost + 3 * (size_t)ctx->numItems,
                      order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, S));
     ctx->orderValid[slot] = true;
   }
+  // kernel_ms: the frame's own kernels (camera-ray pass, frame kernel, reorder), so the
+  // policy probe weighs the order's cost too; the running-mean update below is not in it
+  CK(hipEventRecord(eve, S));
   if (piped) {
     // the running-mean update, in frame order: after the previous frame's update and
     // after whatever the caller's stream held when this frame was requested

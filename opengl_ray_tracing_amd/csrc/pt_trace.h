@@ -690,6 +690,32 @@ struct TileCursor {
     }
     return -1;
   }
+  // Claim ahead (PT_CLAIM_AHEAD): the home queue's next slot is claimed when a
+  // tile starts and resolved when it ends, so the device-scope atomic's round
+  // trip overlaps the tile's own fetches instead of preceding them.
+  int ahead = -1;  // lane 0: the claimed slot of queue (home + qi), -1 = none outstanding
+  __device__ __forceinline__ void claimAhead(int* queue, int home) {
+    if (qi < NUM_QUEUES && (threadIdx.x & 63) == 0)
+      ahead = atomicAdd(queue + ((home + qi) & (NUM_QUEUES - 1)) * CTL_LINE_INTS, 1);
+  }
+  __device__ __forceinline__ int nextAhead(int* queue, int perQueue, int numItems, int home, const int* order,
+                                           int orderCap) {
+    if (qi < NUM_QUEUES) {
+      const int it = __shfl(ahead, 0, 64);
+      ahead = -1;
+      if (it >= 0) {
+        const int q = (home + qi) & (NUM_QUEUES - 1);
+        if (order) {
+          if (it < order[NUM_QUEUES * orderCap + q]) return order[q * orderCap + it];
+        } else {
+          const int t = q * perQueue + it;
+          if (it < perQueue && t < numItems) return t;
+        }
+        qi++;
+      }
+    }
+    return next(queue, perQueue, numItems, home, order, orderCap);
+  }
 };
 
 // per-wave sum of a lane counter into the block's padded shard

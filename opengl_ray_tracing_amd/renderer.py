@@ -36,6 +36,7 @@ FLAG_SERIAL_FRAMES = 0x80
 FLAG_NO_BINS = 0x100
 FLAG_HOST_ACCEL = 0x200
 FLAG_MEGAKERNEL = 0x400
+FLAG_PRIMARY_PASS = 0x800
 GATHER = {"auto": 0, "copy": 1, "rccl": 2}
 
 

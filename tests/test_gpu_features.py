@@ -332,7 +332,7 @@ def test_camera_restart_keeps_policies_and_restarts_the_mean(name):
     with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce) as r:
         r.upload_scene(tris, nodes)
         r.upload_env(hdr)
-        for f in range(20):  # past the 14-frame policy probe
+        for f in range(24):  # past the 20-frame policy probe
             r.render_frame(*a, f)
         tree = r.stats().runtime_tree
         for f in range(3):
@@ -346,3 +346,30 @@ def test_camera_restart_keeps_policies_and_restarts_the_mean(name):
             r.render_frame(*b, f)
         fresh = r.accum()
     assert np.array_equal(moved, fresh)
+
+
+@pytest.mark.parametrize("name", ["c2", "c4"])
+def test_band_order_frames_equal_ordered_frames(name):
+    """Frames handed out in band order (PT_FLAG_NO_TILE_ORDER, and the probe's band-order trial
+    frames 15-16 of pt_runtime.cpp probePolicy) give the longest-first frames' image bit for bit,
+    across the probe and a camera restart."""
+    from opengl_ray_tracing_amd import FLAG_NO_TILE_ORDER
+    cfg, tris, nodes, hdr = scenes.build_config(name)
+    w, h = 480, 270
+    a = orbit_camera(*cfg.camera)
+    b = orbit_camera(cfg.camera[0] + 7.0, cfg.camera[1] + 3.0, cfg.camera[2])
+
+    def run(flags):
+        with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=flags) as r:
+            r.upload_scene(tris, nodes)
+            r.upload_env(hdr)
+            for f in range(24):
+                r.render_frame(*a, f, sync=False)
+            first = r.accum()
+            for f in range(4):
+                r.render_frame(*b, f, sync=False)
+            return first, r.accum(), r.stats().rays
+
+    x, y = run(0), run(FLAG_NO_TILE_ORDER)
+    assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1])
+    assert x[2] == y[2]

@@ -35,7 +35,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "gpurun_out"
-PROBE = 14
+PROBE = 20
 TRACE_RUN = (5, 30)    # tools/gpu_profile.sh: --warmup 5 --steps 30 under --kernel-trace
 COUNTER_RUN = (2, 10)  # --warmup 2 --steps 10 under each --pmc pass
 BENCH_KERNEL = re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true(, \d+)?(, (true|false))?>")

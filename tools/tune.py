@@ -59,7 +59,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--builder", default=None)
     ap.add_argument("--frames", type=int, default=40)
-    ap.add_argument("--warmup", type=int, default=16)  # > the renderer's 13-frame policy probe
+    ap.add_argument("--warmup", type=int, default=22)  # > the renderer's 19-frame policy probe
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--child", default=None)
     ap.add_argument("--max-bounce", type=int, default=None)
