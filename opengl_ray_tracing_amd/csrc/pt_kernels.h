@@ -85,6 +85,9 @@ constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
 // 1 = without (c3 0.257, c2 0.380), 0 = the binary runtime tree
 #define PT_WIDE4 2
 #endif
+#ifndef PT_STATIC_PCT
+#define PT_STATIC_PCT 0  // megakernel in band order: % of the tiles dealt to the waves statically
+#endif
 #ifndef PT_CLAIM_AHEAD
 #define PT_CLAIM_AHEAD 0  // megakernel: claim the next tile when a tile starts (TileCursor::claimAhead)
 #endif
@@ -180,7 +183,11 @@ struct RenderParams {
   // PRIM_TILE (the tile's bin is over PT_BIN_CAP: the megakernel traces the tile's
   // packet); null = the megakernel traces its camera rays itself
   int2* primHit;
-  int* queue;          // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
+  // band order (tileOrder null): items [0, staticItems) are dealt without atomics, wave w of
+  // the grid taking w, w + waves, ...; the rest, staticItems + q * dynPerQueue + i, are
+  // claimed from queue q as usual (staticItems 0: every item claimed)
+  int staticItems, dynPerQueue;
+  int* queue;           // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
   int perQueue;         // items per queue
   int numItems;         // 8x8 wave tiles owned by this rank
   int shardSize;        // shard tile edge (multiple of 8)

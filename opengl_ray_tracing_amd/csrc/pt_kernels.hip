@@ -828,7 +828,21 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   // queue and running them 64 at a time keeps every lane busy, but it mixes
   // tiles: 64-path batches made c2 0.77 ms instead of 0.55, 32-path batches
   // 0.59 -- the coherence of one tile's rays is worth more than full lanes.)
-  int item = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+  const int waveId = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6), numWaves = gridDim.x * (BLOCK / 64);
+  int dealt = 0;  // statically dealt items taken (band order)
+  auto claim = [&]() -> int {
+    if (p.staticItems > 0) {
+      const int t = waveId + dealt * numWaves;
+      if (t < p.staticItems) {
+        dealt++;
+        return t;
+      }
+      const int it = cur.next(p.queue, p.dynPerQueue, p.numItems - p.staticItems, home);
+      return it < 0 ? it : p.staticItems + it;
+    }
+    return cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+  };
+  int item = claim();
   while (item >= 0) {
 #if PT_CLAIM_AHEAD
     cur.claimAhead(p.queue, home);
@@ -895,7 +909,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
 #if PT_CLAIM_AHEAD
     item = cur.nextAhead(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
 #else
-    item = cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+    item = claim();
 #endif
   }
 #if PT_WAVE_TRACE

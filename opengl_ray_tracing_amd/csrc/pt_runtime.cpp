@@ -1589,6 +1589,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.orderCap = orderCap;
   p.tileCost = orderedNow ? cost : nullptr;
   p.tileCostMax = orderedNow ? cost + ctx->numItems : nullptr;
+  if (!orderedNow && !regen && !count && PT_STATIC_PCT > 0) {
+    p.staticItems = (int)((long long)ctx->numItems * PT_STATIC_PCT / 100);
+    p.dynPerQueue = (ctx->numItems - p.staticItems + NUM_QUEUES - 1) / NUM_QUEUES;
+  }
   // While the policy probe times frames (PT_SPLIT_AUTO, 20 frames after a restart)
   // a pipelined frame still starts only after the previous one has ended.
   const bool probing = ordered && PT_SPLIT_AUTO &&
