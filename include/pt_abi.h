@@ -55,8 +55,10 @@ extern "C" {
 #define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */
 #define PT_FLAG_SERIAL_FRAMES 0x80u /* megakernel: no frames in flight (each frame starts after the previous one ends) */
 #define PT_FLAG_NO_BINS 0x100u    /* megakernel: camera rays walk the BVH (no per-tile camera-ray bins) */
-#define PT_FLAG_PRIMARY_PASS 0x800u /* megakernel: camera rays traced by a one-wave-per-tile pass before the
-                                       megakernel instead of inside it (same images; slower on c2-c4) */
+#define PT_FLAG_PRIMARY_PASS 0x800u /* camera rays traced by a one-wave-per-tile pass (camera-ray bins) before
+                                       the frame kernel instead of inside it: same images; the default for
+                                       the large-scene regen kernel (c5 -9 %), slower for the megakernel
+                                       on c2-c4. PT_FLAG_NO_BINS turns the pass off */
 #define PT_FLAG_MEGAKERNEL 0x400u /* large scenes (> 48 MB of records): the lock-step megakernel instead of
                                      the path-regeneration kernel the Disney/MIS integrators default to there */
 #define PT_FLAG_HOST_ACCEL 0x200u /* pt_upload_scene builds the runtime's own tree on the host (threaded binned

@@ -283,6 +283,18 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
           s.py = py;
           startPath(p, s);
           active = true;
+          if (p.primHit) {  // the camera ray's result from the camera-ray pass (primaryKernel)
+            const int2 h = p.primHit[(size_t)py * p.width + px];
+            if (h.x == PRIM_MISS) {
+              active = false;  // a sky pixel, finished by the pass: the lane takes another
+            } else if (h.x >= 0) {
+              V3 color;
+              if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
+                writeAccum(p, s.px, s.py, color);
+                active = false;
+              }
+            }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
+          }
         }
       }
       cursor = min(64, cursor + __popcll(idle));

@@ -124,6 +124,10 @@ struct pt_ctx {
   hipStream_t slotStream[PIPE] = {};
   hipEvent_t mixDone[PIPE] = {};            // slot's last running-mean update
   hipEvent_t userMark = nullptr;            // the caller's stream at the last frame's call
+  // camera-ray bins built on one slot's stream: binsBuilt is recorded after the build, and
+  // every other slot waits for it once before its first frame with those bins (binGen)
+  hipEvent_t binsBuilt = nullptr;
+  unsigned binGen = 0, binGenSeen[MAX_SLOTS] = {};
   float4* d_col[PIPE] = {};                 // per-slot sample colours
   int2* d_prim[PIPE] = {};                  // per-slot camera-ray results (primaryKernel)
   int lastSlot = -1;                        // slot of the last pipelined frame
@@ -303,6 +307,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
       CKC(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
       CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
     }
+    CKC(hipEventCreateWithFlags(&ctx->binsBuilt, hipEventDisableTiming));
   }
 #undef CKC
   *out = ctx;
@@ -376,6 +381,7 @@ void pt_destroy(pt_ctx* ctx) {
     if (ctx->slotStream[k]) (void)hipStreamDestroy(ctx->slotStream[k]);
   }
   if (ctx->userMark) (void)hipEventDestroy(ctx->userMark);
+  if (ctx->binsBuilt) (void)hipEventDestroy(ctx->binsBuilt);
   freeWavefront(ctx);
   for (hipEvent_t e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1560,7 +1566,12 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // camera-ray bins, rebuilt when the camera or the scene changed (the previous frame
   // has ended first: it may still read the old bins); they need the reference facts
   // refReachable checks a bin's winner against
-  const bool bins = PT_BINS && !regen && !count && ctx->fastReady && !(c.flags & PT_FLAG_NO_BINS);
+  // The camera-ray pass (primaryKernel) traces the camera rays ahead of the frame kernel: on
+  // request, and by default for the large-scene regen kernel (c5 7.52 -> 6.86 ms), whose lanes
+  // then start from the camera ray's hit; the megakernel is faster with its camera rays inside
+  // (c2 0.372 vs 0.383 ms with the pass)
+  const bool pass = (c.flags & PT_FLAG_PRIMARY_PASS) || (regen && wide);
+  const bool bins = PT_BINS && !count && ctx->fastReady && !(c.flags & PT_FLAG_NO_BINS) && (!regen || pass);
   if (bins) {
     if (!ctx->binsValid || ctx->binVersion != ctx->sceneVersion || std::memcmp(ctx->binEye, eye, sizeof(ctx->binEye)) ||
         std::memcmp(ctx->binCam, cameraRotate, sizeof(ctx->binCam))) {
@@ -1571,13 +1582,22 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
       std::memcpy(ctx->binCam, cameraRotate, sizeof(ctx->binCam));
       ctx->binVersion = ctx->sceneVersion;
       ctx->binsValid = true;
+      if (piped) {
+        CK(hipEventRecord(ctx->binsBuilt, S));
+        ctx->binGen++;
+        ctx->binGenSeen[slot] = ctx->binGen;
+      }
+    }
+    // a frame in flight on the other slot's stream must not read bins still being built
+    if (piped && ctx->binGenSeen[slot] != ctx->binGen) {
+      CK(hipStreamWaitEvent(S, ctx->binsBuilt, 0));
+      ctx->binGenSeen[slot] = ctx->binGen;
     }
     p.binStart = ctx->bins.binStart;
     p.binTris = ctx->bins.binTris;
     p.binTilesX = ctx->bins.tilesX;
     p.binTilesY = ctx->bins.tilesY;
-    // the camera-ray pass (primaryKernel) ahead of the megakernel, on request
-    if (c.flags & PT_FLAG_PRIMARY_PASS) {
+    if (pass) {
       if (!ctx->d_prim[slot]) CK(hipMalloc(&ctx->d_prim[slot], npix * sizeof(int2)));
       p.primHit = ctx->d_prim[slot];
     }

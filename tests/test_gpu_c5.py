@@ -15,7 +15,7 @@ import pytest
 
 import oracle
 import parity
-from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_REFERENCE_TREE, Renderer, orbit_camera, scenes
+from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_NO_BINS, FLAG_REFERENCE_TREE, Renderer, orbit_camera, scenes
 
 pytestmark = pytest.mark.gpu
 
@@ -61,6 +61,10 @@ def test_c5_full_workload_binned_tree():
     assert sm.regen == 0 and sm.waves_per_simd == 3
     b, sb = render(cfg, tris, nodes, hdr, flags=FLAG_MEGAKERNEL | FLAG_REFERENCE_TREE)
     assert np.array_equal(g, m) and np.array_equal(m, b) and sm.rays == sb.rays
+    # the default regen frame takes its camera rays from the camera-ray pass; without it
+    # (no bins) the regen kernel traces them itself: the same image and rays
+    n, sn = render(cfg, tris, nodes, hdr, flags=FLAG_NO_BINS)
+    assert sn.regen == 1 and np.array_equal(g, n) and sn.rays == st.rays
     px = parity.sample_pixels(cfg.width, cfg.height, 2000, seed=5)
     s = parity.assert_parity(g[px[:, 1], px[:, 0]], oracle_pixels(cfg, tris, nodes, hdr, px), "c5/binned")
     print("c5 binned", s, "rays", st.rays)

@@ -315,14 +315,16 @@ def test_camera_bins_equal_bvh_camera_rays(request, name, integrator, tile):
     assert sa.rays == sb.rays
 
 
-@pytest.mark.parametrize("name,integrator,tile", [("c2", "lambert", (0, 1)), ("c4", "mis", (0, 1)),
-                                                  ("c3", "disney", (1, 3))])
-def test_camera_ray_pass_equals_megakernel_camera_rays(request, name, integrator, tile):
-    """The camera-ray pass (primaryKernel, one wave per tile before the megakernel; the
-    default) gives the images and ray counts of camera rays traced inside the megakernel
-    (PT_FLAG_PRIMARY_PASS) bit for bit: near and far cameras (the far one fills bins past
-    PT_BIN_CAP, whose tiles the megakernel traces as packets), a camera move and a shard."""
-    from opengl_ray_tracing_amd import FLAG_PRIMARY_PASS
+@pytest.mark.parametrize("name,integrator,tile,regen", [("c2", "lambert", (0, 1), False), ("c4", "mis", (0, 1), False),
+                                                        ("c3", "disney", (1, 3), False), ("c4", "mis", (0, 1), True),
+                                                        ("c3", "disney", (1, 3), True)])
+def test_camera_ray_pass_equals_megakernel_camera_rays(request, name, integrator, tile, regen):
+    """The camera-ray pass (primaryKernel, one wave per tile before the frame kernel,
+    PT_FLAG_PRIMARY_PASS) gives the images and ray counts of camera rays traced inside the
+    megakernel / the path-regeneration kernel bit for bit: near and far cameras (the far one
+    fills bins past PT_BIN_CAP, whose tiles the frame kernel traces itself), a camera move and
+    a shard."""
+    from opengl_ray_tracing_amd import FLAG_PRIMARY_PASS, FLAG_REGEN
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     cams = [orbit_camera(*cfg.camera), orbit_camera(40.0, 25.0, 1.5), orbit_camera(-70.0, -10.0, 14.0)]
     w, h = 960, 540
@@ -339,8 +341,9 @@ def test_camera_ray_pass_equals_megakernel_camera_rays(request, name, integrator
                 out.append(r.accum())
             return out, r.stats()
 
-    a, sa = run(0)
-    b, sb = run(FLAG_PRIMARY_PASS)
+    base = FLAG_REGEN if regen else 0
+    a, sa = run(base)
+    b, sb = run(base | FLAG_PRIMARY_PASS)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert sa.rays == sb.rays
