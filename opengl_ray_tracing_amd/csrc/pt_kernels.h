@@ -237,6 +237,9 @@ struct PackParams {
 #ifndef PT_BIN_CAP
 #define PT_BIN_CAP 32  // a tile whose bin holds more triangles traces its camera rays through the BVH
 #endif
+#ifndef PT_PASS_BIN_CAP
+#define PT_PASS_BIN_CAP PT_BIN_CAP  // the camera-ray pass (primaryKernel): its own cap, staged per one-wave block
+#endif
 #ifndef PT_BINS
 #define PT_BINS 1      // 0: no camera-ray bins
 #endif

@@ -411,8 +411,8 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
 // waves per SIMD in flight and claims nothing. Sky pixels are finished here;
 // every other pixel's result goes to primHit for the megakernel.
 __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
-  __shared__ float4 s_tri[PT_BIN_CAP * 4];
-  __shared__ int s_idx[PT_BIN_CAP];
+  __shared__ float4 s_tri[PT_PASS_BIN_CAP * 4];
+  __shared__ int s_idx[PT_PASS_BIN_CAP];
   const int w = blockIdx.x;
   const int lane = threadIdx.x;
   const int sub = p.shardSize >> 3;
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   }
   const int n = b1 - b0;
   int2* out = p.primHit + (size_t)py * p.width + px;
-  if (n > PT_BIN_CAP) {  // the megakernel traces this tile's camera rays as a packet
+  if (n > PT_PASS_BIN_CAP) {  // the frame kernel traces this tile's camera rays (the megakernel as a packet)
     if (valid) *out = make_int2(PRIM_TILE, 0);
     return;
   }
