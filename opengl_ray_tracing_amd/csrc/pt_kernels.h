@@ -238,7 +238,7 @@ struct PackParams {
 #define PT_BIN_CAP 32  // a tile whose bin holds more triangles traces its camera rays through the BVH
 #endif
 #ifndef PT_PASS_BIN_CAP
-#define PT_PASS_BIN_CAP PT_BIN_CAP  // the camera-ray pass (primaryKernel): its own cap, staged per one-wave block
+#define PT_PASS_BIN_CAP 64  // the camera-ray pass (primaryKernel), staged per one-wave block: c5 32 6.84, 64 6.77, 128 6.79, 256 7.08 ms
 #endif
 #ifndef PT_BINS
 #define PT_BINS 1      // 0: no camera-ray bins
