@@ -284,17 +284,20 @@ def make_roofline(args, cfg, kernel_ms, rays_per_launch, bytes_per_ray, n):
             **base}
 
 
-REF_PSNR_128SPP = 20.71  # the reference CPU tracer at 128 spp vs its 4000spp.png
-
-
 def spp_matched_psnr(device: int, spp: int = 128):
     """The metric's "CPU-ref spp-matched PSNR": the BasicRayTracingWithC++ scene (config c1, 256x256)
-    rendered by the GPU BASIC_CPU_COMPAT integrator at 128 spp, imshow'd (main.cpp:169-190) and
-    compared with the reference's own 4000 spp image; the reference at 128 spp scores 20.71 dB."""
+    rendered by the GPU BASIC_CPU_COMPAT integrator at 128 spp, imshow'd (main.cpp:183) and
+    compared with the reference's own 4000 spp image, beside what the reference CPU tracer itself
+    scores at 128 spp (tests/golden/basic/ref_s128.json: that program compiled from its source,
+    std::mt19937 seeded 5489)."""
+    import json
+
     from PIL import Image
 
     from opengl_ray_tracing_amd import Renderer, scenes
+    from opengl_ray_tracing_amd.scene import imshow_bytes
     gold = ROOT / "tests" / "golden" / "4000spp.png"
+    fix = ROOT / "tests" / "golden" / "basic" / f"ref_s{spp}.json"
     if not gold.exists():
         return None
     with Renderer(256, 256, "basic", basic_samples=spp, device=device) as r:
@@ -305,11 +308,12 @@ def spp_matched_psnr(device: int, spp: int = 128):
             r.render_frame(z, eye4, k, sync=False)
         r.synchronize()
         dt = time.perf_counter() - t0
-        acc = r.accum()
-    img = np.clip(np.power(np.maximum(acc[..., :3].astype(np.float64), 0), 1 / 2.2) * 255, 0, 255).astype(np.uint8)
+        img = imshow_bytes(r.basic_image())
     ref = np.asarray(Image.open(gold))[..., :3].astype(np.float64)
     psnr = 10 * np.log10(255.0 ** 2 / np.mean((img.astype(np.float64) - ref) ** 2))
-    return {"psnr_db": round(float(psnr), 2), "reference_psnr_db": REF_PSNR_128SPP, "spp": spp,
+    ref_psnr = json.loads(fix.read_text())["psnr_vs_4000spp_db"] if fix.exists() else None
+    return {"psnr_db": round(float(psnr), 2), "reference_psnr_db": None if ref_psnr is None else round(ref_psnr, 2),
+            "reference_source": str(fix.relative_to(ROOT)), "spp": spp,
             "scene": "c1 BasicRayTracingWithC++ Cornell box 256x256", "vs": "4000spp.png (reference)",
             "render_ms": round(dt * 1e3, 2)}
 

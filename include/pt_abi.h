@@ -26,8 +26,9 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 3  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
-                             3: scene-upload fields at the end of pt_frame_stats, pt_build_bvh_device */
+#define PT_ABI_VERSION 4  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
+                             3: scene-upload fields at the end of pt_frame_stats, pt_build_bvh_device;
+                             4: BASIC shapes as doubles, its double image, the replayed random stream */
 
 /* error codes */
 #define PT_OK 0
@@ -149,8 +150,26 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int nTriangles, const float*
  * library computes it). hdrResolution := w. hdr == NULL clears the env (black). */
 int pt_upload_env(pt_ctx* ctx, const float* hdr, int w, int h, const float* cache);
 
-/* PT_BASIC_CPU_COMPAT shape list: n x 24 f32 records (layout in pt_scene.h). */
-int pt_upload_shapes(pt_ctx* ctx, const float* shapes, int n);
+/* PT_BASIC_CPU_COMPAT shape list (the vector<Shape*> of BasicRayTracingWithC++/main.cpp:306-353):
+ * n x 24 f64 records (layout in pt_scene.h; the reference's Material rates and sphere radius
+ * are doubles, its vec3 fields floats). */
+int pt_upload_shapes(pt_ctx* ctx, const double* shapes, int n);
+
+/* PT_BASIC_CPU_COMPAT: the reference's `double* image` (BasicRayTracingWithC++/main.cpp:356,
+ * summed by :427-429; row 0 = top), width x height x 3 f64 host buffer. The f32 accumulation
+ * (pt_download_accum) holds the same sums rounded to float. */
+int pt_download_basic_image(pt_ctx* ctx, double* rgb);
+
+/* PT_BASIC_CPU_COMPAT: replay a recorded random stream instead of the per-pixel counter RNG,
+ * so a frame consumes exactly the random numbers the reference's serial run consumed
+ * (its one global std::mt19937 read by randf(), main.cpp:208-214). stream = n doubles in
+ * draw order; offsets[(k * height + i) * width + j] = the stream position at which sample k
+ * of pixel (row i from the top, column j) starts (n_offsets = samples * width * height; a
+ * sample's draws end where the next one's start). A pixel sample that would read past its
+ * end gets 0.5 and is counted (pt_basic_replay_overruns). stream == NULL switches back to
+ * the counter RNG. Frame frameCounter renders sample k = frameCounter. */
+int pt_set_basic_stream(pt_ctx* ctx, const double* stream, int64_t n, const int64_t* offsets, int64_t n_offsets);
+int pt_basic_replay_overruns(pt_ctx* ctx, int64_t* count);
 
 /* calculateHdrCache (ImportanceSampling_LowDiscrepancySequence/main.cpp:555-652)
  * computed on this context's GPU; output as pt_hdr_cache (w*h*3 f32: sample x,

@@ -67,8 +67,13 @@ void pt_free(void* p);
 /* calculateHdrCache (ImportanceSampling_LowDiscrepancySequence/main.cpp:555-652). */
 int pt_hdr_cache(const float* hdr, int w, int h, float* cache_out);
 
-/* BASIC_CPU_COMPAT shape records (24 f32 each, see oracle/pt_oracle.h). */
-#define PT_SHAPE_FLOATS 24
+/* BASIC_CPU_COMPAT shape records, 24 f64 each (BasicRayTracingWithC++/main.cpp:42-165):
+ * [0] type (0 triangle, 1 sphere), [1..3] p1 or sphere centre, [4..6] p2, [7..9] p3,
+ * [10..12] color, [13..15] triangle normal normalize(cross(p2-p1, p3-p1)) (:85),
+ * [16] isEmissive, [17] specularRate, [18] roughness, [19] refractRate,
+ * [20] refractAngle, [21] refractRoughness, [22] sphere radius, [23] unused.
+ * The vec3 fields hold float values (glm vec3), the rates and the radius doubles. */
+#define PT_SHAPE_DOUBLES 24
 
 /* Image output. The GL demos only display; BasicRayTracingWithC++ writes its
  * image with imshow + svpng (main.cpp:169-190). pixels: h rows of w pixels of

@@ -40,7 +40,7 @@ CXX_FLAGS = ["-O2", "-fPIC", "-pthread", "-std=c++17", "-ffp-contract=off", "-fn
              "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"]
 
 SOURCES = {
-    "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h", CSRC / "pt_trace.h",
+    "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h", CSRC / "pt_trace.h", INCLUDE / "pt_scene.h",
                                                        INCLUDE / "pt_fmath.h"]),
     "pt_wavefront.o": ("hip", CSRC / "pt_wavefront.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h",
                                                            CSRC / "pt_trace.h", CSRC / "pt_wavefront.h",

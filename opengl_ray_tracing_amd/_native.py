@@ -13,8 +13,9 @@ from . import _build
 
 _lib = None
 
-ABI_VERSION = 3  # include/pt_abi.h PT_ABI_VERSION
+ABI_VERSION = 4  # include/pt_abi.h PT_ABI_VERSION
 c_float_p = C.POINTER(C.c_float)
+c_double_p = C.POINTER(C.c_double)
 c_int_p = C.POINTER(C.c_int)
 
 
@@ -60,7 +61,10 @@ SIGNATURES = {
     "pt_last_error": (C.c_char_p, [C.c_void_p]),
     "pt_upload_scene": (C.c_int, [C.c_void_p, c_float_p, C.c_int, c_float_p, C.c_int]),
     "pt_upload_env": (C.c_int, [C.c_void_p, c_float_p, C.c_int, C.c_int, c_float_p]),
-    "pt_upload_shapes": (C.c_int, [C.c_void_p, c_float_p, C.c_int]),
+    "pt_upload_shapes": (C.c_int, [C.c_void_p, c_double_p, C.c_int]),
+    "pt_download_basic_image": (C.c_int, [C.c_void_p, c_double_p]),
+    "pt_set_basic_stream": (C.c_int, [C.c_void_p, c_double_p, C.c_int64, C.POINTER(C.c_int64), C.c_int64]),
+    "pt_basic_replay_overruns": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
     "pt_render_frame": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32, c_float_p]),
     "pt_render_frame_async": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32]),
     "pt_trace_closest": (C.c_int, [C.c_void_p, c_float_p, C.c_int, c_float_p, c_int_p]),

@@ -217,15 +217,23 @@ struct TraceParams {
   int ovfDepth;
 };
 
+// BasicRayTracingWithC++ (pt_kernels.hip basicKernel): one sample k of every pixel
+constexpr int BASIC_MAX_DEPTH = 31;  // pathTracing vertices kept for the fold (the reference's cutoff is 8)
 struct BasicParams {
-  const float* shapes;
+  const double* shapes;         // nShapes x PT_SHAPE_DOUBLES
   int nShapes;
   int width, height;
-  uint32_t sample, seed;
+  uint32_t sample, seed;        // k, and the counter RNG's run seed
   int maxDepth;
-  float brightness;
-  float4* accum;
-  unsigned long long* stats;
+  int reset;                    // frameCounter == 0: this sample starts the image
+  float brightness;             // BRIGHTNESS (B:20) as glm's operator*= casts it
+  float4* accum;                // the image as f32 (pt_download_accum)
+  double* image;                // the reference's double image, width x height x 3 (B:356)
+  const double* stream;         // replayed randf() stream (nullable: counter RNG)
+  const long long* offsets;     // replay: start of each sample's draws, (k * height + i) * width + j
+  long long streamN, nOffsets;
+  unsigned long long* stats;    // ray counter
+  unsigned long long* overruns; // replay: pixel samples that read past their draws
 };
 
 struct PackParams {

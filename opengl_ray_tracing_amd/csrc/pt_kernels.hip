@@ -22,6 +22,7 @@
 
 #include "pt_device.h"
 #include "pt_kernels.h"
+#include "pt_scene.h"
 #include "pt_trace.h"
 
 namespace pt {
@@ -497,22 +498,44 @@ __device__ __forceinline__ void finishPixel(const RenderParams& p, int px, int p
 }
 
 // ------------------------------------------------ BASIC (BasicRayTracingWithC++)
+// The reference binary's arithmetic (oracle/pt_oracle.c b_*, pinned byte for byte
+// against the reference compiled from its source): glm vec3 is float, the Material
+// rates, the sphere radius, HitResult::distance and the image are double
+// (B:49-68, :130, :356), each mixed expression in the type C++ promotes it to.
 struct BHit {
-  float distance;
+  double distance;
   V3 P, N, color;
   bool emissive;
-  float specularRate, roughness, refractRate, refractAngle, refractRoughness;
+  double specularRate, roughness, refractRate, refractAngle, refractRoughness;
 };
-// Triangle::intersect B:90-122 / Sphere::intersect B:135-164
-__device__ __forceinline__ bool bIntersect(const float* sh, V3 S, V3 d, BHit& res) {
-  if (sh[0] == 1.0f) {
-    V3 O = ld3(sh + 1);
-    float R = sh[22];
-    float OS = sqrtf(dot(O - S, O - S));
-    float SH = dot(O - S, d);
-    float OH = sqrtf(OS * OS - SH * SH);
-    if (OH > R) return false;
-    float PH = sqrtf(R * R - OH * OH);
+// randf B:211-214: the per-pixel counter stream, or the replayed reference stream
+struct BRng {
+  uint32_t seed;
+  const double* rep;
+  long long pos, end;
+  bool over;
+};
+__device__ __forceinline__ double bRand(BRng& g) {
+  if (g.rep) {
+    if (g.pos < g.end) return g.rep[g.pos++];
+    g.over = true;
+    return 0.5;
+  }
+  return (double)wang(g.seed) / 4294967296.0;
+}
+__device__ __forceinline__ V3 ldf3(const double* p) { return v3((float)p[0], (float)p[1], (float)p[2]); }
+// Triangle::intersect B:90-122 / Sphere::intersect B:135-164 (OS, SH, t float; pow(x, 2)
+// of a float exact in double; R double, so OH > R and PH double expressions)
+__device__ __forceinline__ bool bIntersect(const double* sh, V3 S, V3 d, BHit& res) {
+  if (sh[0] == 1.0) {
+    V3 O = ldf3(sh + 1);
+    double R = sh[22];
+    V3 OSv = O - S;
+    float OS = sqrtf(dot(OSv, OSv));
+    float SH = dot(OSv, d);
+    float OH = (float)sqrt((double)OS * (double)OS - (double)SH * (double)SH);
+    if ((double)OH > R) return false;
+    float PH = (float)sqrt(R * R - (double)OH * (double)OH);
     float t1 = fabsf(SH) - PH;
     float t2 = fabsf(SH) + PH;
     float t = (t1 < 0) ? t2 : t1;
@@ -522,7 +545,7 @@ __device__ __forceinline__ bool bIntersect(const float* sh, V3 S, V3 d, BHit& re
     res.P = P;
     res.N = normalize(P - O);
   } else {
-    V3 p1 = ld3(sh + 1), p2 = ld3(sh + 4), p3 = ld3(sh + 7), n = ld3(sh + 13);
+    V3 p1 = ldf3(sh + 1), p2 = ldf3(sh + 4), p3 = ldf3(sh + 7), n = ldf3(sh + 13);
     V3 N = n;
     if (dot(N, d) > 0.0f) N = -N;
     if (fabsf(dot(N, d)) < 0.00001f) return false;
@@ -535,48 +558,57 @@ __device__ __forceinline__ bool bIntersect(const float* sh, V3 S, V3 d, BHit& re
     res.P = P;
     res.N = N;
   }
-  res.color = ld3(sh + 10);
-  res.emissive = sh[16] != 0.0f;
+  res.color = ldf3(sh + 10);
+  res.emissive = sh[16] != 0.0;
   res.specularRate = sh[17]; res.roughness = sh[18]; res.refractRate = sh[19];
   res.refractAngle = sh[20]; res.refractRoughness = sh[21];
   return true;
 }
-// shoot B:192-205
-__device__ __forceinline__ bool bShoot(const float* shapes, int n, V3 S, V3 d, BHit& best) {
+// shoot B:192-205 (res.distance a double initialised from 1145141919.810f)
+__device__ __forceinline__ bool bShoot(const double* shapes, int n, V3 S, V3 d, BHit& best) {
   bool any = false;
-  best.distance = 1145141919.810f;
+  best.distance = (double)1145141919.810f;
   for (int k = 0; k < n; k++) {
     BHit r;
-    if (bIntersect(shapes + (size_t)k * 24, S, d, r) && r.distance < best.distance) {
+    if (bIntersect(shapes + (size_t)k * PT_SHAPE_DOUBLES, S, d, r) && r.distance < best.distance) {
       best = r;
       any = true;
     }
   }
   return any;
 }
-// randomDirection B:237-250
-__device__ __forceinline__ V3 bRandomDirection(V3 n, uint32_t& seed) {
+// randomVec3 B:217-234 (the compiled reference evaluates vec3(randf(), randf(), randf())
+// right to left: z takes the first draw) / randomDirection B:237-250
+__device__ __forceinline__ V3 bRandomDirection(V3 n, BRng& g) {
   V3 dd;
   do {
-    float a = randf(seed), b = randf(seed), c = randf(seed);
-    dd = v3(a, b, c) * 2.0f - v3(1, 1, 1);
-  } while (dot(dd, dd) > 1.0f);
+    double z = bRand(g), y = bRand(g), x = bRand(g);
+    dd = v3((float)x, (float)y, (float)z) * 2.0f - v3(1, 1, 1);
+  } while ((double)dot(dd, dd) > 1.0);
   return normalize(normalize(dd) + n);
 }
-__device__ __forceinline__ V3 bRefract(V3 I, V3 N, float eta) {  // glm refract
+// glm reflect / refract (func_geometric.inl:104-123), glm mix(vec3, vec3, double) in double
+__device__ __forceinline__ V3 bReflect(V3 I, V3 N) { return I - (N * dot(N, I)) * 2.0f; }
+__device__ __forceinline__ V3 bRefract(V3 I, V3 N, float eta) {
   float dv = dot(N, I);
   float k = 1.0f - eta * eta * (1.0f - dv * dv);
-  if (k < 0.0f) return v3(0, 0, 0);
+  if (!(k >= 0.0f)) return v3(0, 0, 0);
   return I * eta - N * (eta * dv + sqrtf(k));
 }
-__device__ __forceinline__ int bLobe(const BHit& res, V3 din, uint32_t& seed, V3& dout) {
-  V3 rd = bRandomDirection(res.N, seed);
-  float r = randf(seed);
+__device__ __forceinline__ V3 bMixd(V3 x, V3 y, double a) {
+  const double b = 1.0 - a;
+  return v3((float)((double)x.x * b + (double)y.x * a), (float)((double)x.y * b + (double)y.y * a),
+            (float)((double)x.z * b + (double)y.z * a));
+}
+// lobe choice + new direction (B:399-422, B:268-294): 0 specular, 1 refract, 2 diffuse
+__device__ __forceinline__ int bLobe(const BHit& res, V3 din, BRng& g, V3& dout) {
+  V3 rd = bRandomDirection(res.N, g);
+  double r = bRand(g);
   if (r < res.specularRate) {
-    dout = mixv(normalize(reflect3(din, res.N)), rd, res.roughness);
+    dout = bMixd(normalize(bReflect(din, res.N)), rd, res.roughness);
     return 0;
   } else if (res.specularRate <= r && r <= res.refractRate) {
-    dout = mixv(normalize(bRefract(din, res.N, res.refractAngle)), -rd, res.refractRoughness);
+    dout = bMixd(normalize(bRefract(din, res.N, (float)res.refractAngle)), -rd, res.refractRoughness);
     return 1;
   }
   dout = rd;
@@ -587,14 +619,28 @@ __global__ __launch_bounds__(BLOCK) void basicKernel(BasicParams p) {
   const int j = blockIdx.x * 16 + (threadIdx.x & 15);
   const int i = blockIdx.y * 16 + (threadIdx.x >> 4);
   uint32_t rays = 0;
+  bool over = false;
   if (j < p.width && i < p.height) {
     const int W = p.width, H = p.height;
-    uint32_t seed = ((uint32_t)j * 1973u + (uint32_t)i * 9277u + p.sample * 26699u + p.seed * 0x9E3779B9u) | 1u;
+    BRng g;
+    g.seed = ((uint32_t)j * 1973u + (uint32_t)i * 9277u + p.sample * 26699u + p.seed * 0x9E3779B9u) | 1u;
+    g.rep = p.stream;
+    g.pos = g.end = 0;
+    g.over = false;
+    if (p.stream) {
+      const long long idx = ((long long)p.sample * H + i) * W + j;
+      if (idx < p.nOffsets) {
+        g.pos = p.offsets[idx];
+        g.end = idx + 1 < p.nOffsets ? p.offsets[idx + 1] : p.streamN;
+        g.end = g.end < p.streamN ? g.end : p.streamN;
+      }
+    }
+    // pixel loop body B:367-429
     double xd = 2.0 * (double)j / (double)W - 1.0;
     double yd = 2.0 * (double)(H - i) / (double)H - 1.0;
-    xd += (double)(randf(seed) - 0.5f) / (double)W;
-    yd += (double)(randf(seed) - 0.5f) / (double)H;
-    V3 coord = v3((float)xd, (float)yd, 1.1f);
+    xd += (bRand(g) - 0.5) / (double)W;
+    yd += (bRand(g) - 0.5) / (double)H;
+    V3 coord = v3((float)xd, (float)yd, (float)1.1);  // SCREEN_Z B:27 is a double
     V3 dir = normalize(coord - v3(0, 0, 4.0f));
     BHit res;
     V3 color = v3(0, 0, 0);
@@ -604,36 +650,53 @@ __global__ __launch_bounds__(BLOCK) void basicKernel(BasicParams p) {
         color = res.color;
       } else {
         V3 nd;
-        int lobe = bLobe(res, dir, seed, nd);
-        // pathTracing B:252-297, recursion unrolled into a throughput product
-        V3 S = res.P, d = nd, thr = v3(1, 1, 1), pt = v3(0, 0, 0);
+        int lobe = bLobe(res, dir, g, nd);
+        // pathTracing B:252-297 from depth 0: the recursion forms its products on the way
+        // back up (pathTracing(depth + 1) * cosine [* srcColor] / P), so each vertex's
+        // factors are kept and folded from the deepest vertex upward
+        float cosv[BASIC_MAX_DEPTH + 1];
+        V3 col[BASIC_MAX_DEPTH + 1];
+        bool diff[BASIC_MAX_DEPTH + 1];
+        const float P = 0.8f;  // B:264
+        V3 S = res.P, d = nd, v = v3(0, 0, 0);
+        int n = 0;
         for (int depth = 0; depth <= p.maxDepth; depth++) {
           BHit h;
           rays++;
           if (!bShoot(p.shapes, p.nShapes, S, d, h)) break;
-          if (h.emissive) { pt = thr * h.color; break; }
-          float r = randf(seed);
-          if (r > 0.8f) break;
-          float cosine = fabsf(dot(-d, h.N));
+          if (h.emissive) { v = h.color; break; }
+          double r = bRand(g);
+          if (r > (double)P) break;
           V3 nd2;
-          int lb = bLobe(h, d, seed, nd2);
-          thr = thr * cosine;
-          if (lb == 2) thr = thr * h.color;
-          thr = thr / 0.8f;
+          int lb = bLobe(h, d, g, nd2);
+          cosv[n] = fabsf(dot(-d, h.N));
+          col[n] = h.color;
+          diff[n] = lb == 2;
+          n++;
           S = h.P;
           d = nd2;
         }
-        color = (lobe == 2) ? pt * res.color : pt;
-        color = color * p.brightness;
+        for (int k = n - 1; k >= 0; k--) {
+          v = v * cosv[k];
+          if (diff[k]) v = v * col[k];
+          v = v / P;
+        }
+        color = (lobe == 2) ? v * res.color : v;
+        color = color * p.brightness;  // color *= BRIGHTNESS (glm casts the double to float)
       }
     }
-    float4* a = p.accum + (size_t)i * W + j;
-    float4 o = *a;
-    *a = make_float4(o.x + color.x, o.y + color.y, o.z + color.z, 1.0f);
+    double* im = p.image + 3 * ((size_t)i * W + j);
+    double r0 = p.reset ? 0.0 : im[0], r1 = p.reset ? 0.0 : im[1], r2 = p.reset ? 0.0 : im[2];
+    r0 += color.x; r1 += color.y; r2 += color.z;  // *p += color.x ... (B:427-429)
+    im[0] = r0; im[1] = r1; im[2] = r2;
+    p.accum[(size_t)i * W + j] = make_float4((float)r0, (float)r1, (float)r2, 1.0f);
+    over = g.over;
   }
   // wave-reduce the ray count, one atomic per wave
   for (int off = 32; off > 0; off >>= 1) rays += __shfl_down(rays, off, 64);
   if ((threadIdx.x & 63) == 0 && rays) atomicAdd(reinterpret_cast<unsigned long long*>(p.stats), (unsigned long long)rays);
+  const unsigned long long ov = __ballot(over);
+  if ((threadIdx.x & 63) == 0 && ov) atomicAdd(p.overruns, (unsigned long long)__popcll(ov));
 }
 
 // ------------------------------------------------------------ tile order

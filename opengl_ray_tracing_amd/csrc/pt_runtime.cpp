@@ -97,9 +97,14 @@ struct pt_ctx {
   float4* d_hdr = nullptr;
   float2* d_cache = nullptr;  // sample table (x, y); the pdf lives in d_hdr[k].w
   int hdrW = 0, hdrH = 0;
-  // BASIC shapes
-  float* d_shapes = nullptr;
+  // BASIC shapes, the double image, the replayed random stream
+  double* d_shapes = nullptr;
   int nShapes = 0;
+  double* d_basicImg = nullptr;
+  double* d_stream = nullptr;
+  long long* d_offsets = nullptr;
+  long long streamN = 0, nOffsets = 0;
+  unsigned long long* d_overruns = nullptr;
   // frame state
   float4* d_accum = nullptr;
   // control block (pt_kernels.h CTL_*): padded queue counters (zeroed per
@@ -370,6 +375,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_fbvh); dfree(ctx->d_fbvh4); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri); dfree(ctx->d_refLeafOf);
   dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
+  dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
   freePrimaryBins(ctx->bins);
@@ -1108,16 +1114,59 @@ int pt_hdr_cache_device(pt_ctx* ctx, const float* hdr, int w, int h, float* cach
   return PT_OK;
 }
 
-int pt_upload_shapes(pt_ctx* ctx, const float* shapes, int n) {
+int pt_upload_shapes(pt_ctx* ctx, const double* shapes, int n) {
   if (!ctx || (!shapes && n > 0) || n < 0) return PT_E_INVALID;
   if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "BASIC shapes: one device only");
-  CK(hipSetDevice(ctx->cfg.device_id));
+  if (int rc = syncStreams(ctx)) return rc;
   dfree(ctx->d_shapes);
   ctx->nShapes = 0;
   if (n == 0) return PT_OK;
-  CK(hipMalloc(&ctx->d_shapes, (size_t)n * PT_SHAPE_FLOATS * sizeof(float)));
-  CK(hipMemcpy(ctx->d_shapes, shapes, (size_t)n * PT_SHAPE_FLOATS * sizeof(float), hipMemcpyHostToDevice));
+  CK(hipMalloc(&ctx->d_shapes, (size_t)n * PT_SHAPE_DOUBLES * sizeof(double)));
+  CK(hipMemcpy(ctx->d_shapes, shapes, (size_t)n * PT_SHAPE_DOUBLES * sizeof(double), hipMemcpyHostToDevice));
   ctx->nShapes = n;
+  return PT_OK;
+}
+
+int pt_download_basic_image(pt_ctx* ctx, double* rgb) {
+  if (!ctx || !rgb) return PT_E_INVALID;
+  if (ctx->cfg.integrator != PT_BASIC_CPU_COMPAT) return fail(ctx, PT_E_INVALID, "not a BASIC context");
+  if (int rc = syncStreams(ctx)) return rc;
+  const size_t n = (size_t)ctx->cfg.width * ctx->cfg.height * 3;
+  if (!ctx->d_basicImg) {
+    std::memset(rgb, 0, n * sizeof(double));
+    return PT_OK;
+  }
+  CK(hipMemcpy(rgb, ctx->d_basicImg, n * sizeof(double), hipMemcpyDeviceToHost));
+  return PT_OK;
+}
+
+int pt_set_basic_stream(pt_ctx* ctx, const double* stream, int64_t n, const int64_t* offsets, int64_t nOffsets) {
+  if (!ctx) return PT_E_INVALID;
+  if (ctx->cfg.integrator != PT_BASIC_CPU_COMPAT) return fail(ctx, PT_E_INVALID, "not a BASIC context");
+  if (int rc = syncStreams(ctx)) return rc;
+  dfree(ctx->d_stream);
+  dfree(ctx->d_offsets);
+  ctx->streamN = ctx->nOffsets = 0;
+  if (!stream) return PT_OK;
+  if (n < 1 || !offsets || nOffsets < 1) return fail(ctx, PT_E_INVALID, "pt_set_basic_stream: empty stream or offsets");
+  for (int64_t k = 0; k < nOffsets; k++)
+    if (offsets[k] < 0 || offsets[k] > n || (k > 0 && offsets[k] < offsets[k - 1]))
+      return fail(ctx, PT_E_INVALID, "pt_set_basic_stream: offsets must be non-decreasing within [0, n]");
+  CK(hipMalloc(&ctx->d_stream, (size_t)n * sizeof(double)));
+  CK(hipMalloc(&ctx->d_offsets, (size_t)nOffsets * sizeof(long long)));
+  CK(hipMemcpy(ctx->d_stream, stream, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+  CK(hipMemcpy(ctx->d_offsets, offsets, (size_t)nOffsets * sizeof(long long), hipMemcpyHostToDevice));
+  ctx->streamN = n;
+  ctx->nOffsets = nOffsets;
+  return PT_OK;
+}
+
+int pt_basic_replay_overruns(pt_ctx* ctx, int64_t* count) {
+  if (!ctx || !count) return PT_E_INVALID;
+  if (int rc = syncStreams(ctx)) return rc;
+  unsigned long long v = 0;
+  if (ctx->d_overruns) CK(hipMemcpy(&v, ctx->d_overruns, sizeof(v), hipMemcpyDeviceToHost));
+  *count = (int64_t)v;
   return PT_OK;
 }
 
@@ -1447,6 +1496,17 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   hipEvent_t evb, eve;
   if (c.integrator == PT_BASIC_CPU_COMPAT) {
     if (!ctx->d_shapes) return fail(ctx, PT_E_NOSCENE, "no BASIC shapes uploaded");
+    const int maxDepth = c.max_bounce >= 0 ? c.max_bounce : 8;  // B:254
+    if (maxDepth > BASIC_MAX_DEPTH) return fail(ctx, PT_E_INVALID, "BASIC max_bounce > 31");
+    const size_t npix = (size_t)c.width * c.height;
+    if (!ctx->d_basicImg) {
+      CK(hipMalloc(&ctx->d_basicImg, npix * 3 * sizeof(double)));
+      CK(hipMemsetAsync(ctx->d_basicImg, 0, npix * 3 * sizeof(double), ctx->stream));
+    }
+    if (!ctx->d_overruns) {
+      CK(hipMalloc(&ctx->d_overruns, sizeof(unsigned long long)));
+      CK(hipMemsetAsync(ctx->d_overruns, 0, sizeof(unsigned long long), ctx->stream));
+    }
     int erc = launchEvents(ctx, &evb, &eve);
     if (erc) return erc;
     BasicParams p;
@@ -1456,10 +1516,17 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     p.height = c.height;
     p.sample = sampleIndex(c, frameCounter);
     p.seed = c.basic_seed;
-    p.maxDepth = c.max_bounce >= 0 ? c.max_bounce : 8;
-    p.brightness = (float)((double)(2.0f * 3.1415926f) * (1.0 / (double)c.basic_samples));
+    p.maxDepth = maxDepth;
+    p.reset = frameCounter == 0;
+    p.brightness = (float)((double)(2.0f * 3.1415926f) * (1.0 / (double)c.basic_samples));  // B:20
     p.accum = ctx->d_accum;
+    p.image = ctx->d_basicImg;
+    p.stream = ctx->d_stream;
+    p.offsets = ctx->d_offsets;
+    p.streamN = ctx->streamN;
+    p.nOffsets = ctx->nOffsets;
     p.stats = stats;
+    p.overruns = ctx->d_overruns;
     CK(hipEventRecord(evb, ctx->stream));
     CK(launchBasic(p, ctx->stream));
     CK(hipEventRecord(eve, ctx->stream));
@@ -1666,6 +1733,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     if (ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
     CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[slot], frameCounter, S));
     CK(hipEventRecord(ctx->mixDone[slot], S));
+    // the caller's stream is ordered after this frame (pt_abi.h: stream-ordered calls);
+    // the slot streams' next frame kernels do not wait on it
+    CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[slot], 0));
     ctx->lastSlot = slot;
     ctx->mixPending = true;
     ctx->frameNo++;
@@ -1715,7 +1785,9 @@ int pt_trace_closest(pt_ctx* ctx, const float* rays, int n, float* t_out, int* t
   if (!ctx || n < 0 || (n > 0 && (!rays || !t_out || !tri_out))) return PT_E_INVALID;
   if (!ctx->d_bvh) return fail(ctx, PT_E_NOSCENE, "no scene");
   if (n == 0) return PT_OK;
-  CK(hipSetDevice(ctx->cfg.device_id));
+  // frames in flight read the overflow stack this query reuses (and ensureOverflow may
+  // reallocate): the query runs after every frame issued before it
+  if (int rc = syncStreams(ctx)) return rc;
   if ((size_t)n > ctx->traceCap) {
     dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri);
     CK(hipMalloc(&ctx->d_rays, (size_t)n * 6 * sizeof(float)));
@@ -1792,6 +1864,15 @@ int pt_clear_accum(pt_ctx* ctx) {
     if (hipSetDevice(m->cfg.device_id) != hipSuccess ||
         hipMemsetAsync(m->d_accum, 0, (size_t)m->cfg.width * m->cfg.height * sizeof(float4), m->stream) != hipSuccess)
       return fail(ctx, PT_E_HIP, "pt_clear_accum on device " + std::to_string(m->cfg.device_id));
+    if (m->d_basicImg &&
+        hipMemsetAsync(m->d_basicImg, 0, (size_t)m->cfg.width * m->cfg.height * 3 * sizeof(double), m->stream) != hipSuccess)
+      return fail(ctx, PT_E_HIP, "pt_clear_accum (BASIC image)");
+  }
+  // a group's next gather unpacks into rank 0's accumulation on the gather stream, which
+  // is not ordered after rank 0's stream: the clear completes first
+  if (ctx->gather) {
+    CK(hipSetDevice(ctx->cfg.device_id));
+    CK(hipStreamSynchronize(ctx->stream));
   }
   return PT_OK;
 }

@@ -94,6 +94,8 @@ class Renderer:
         cfg.basic_samples = int(basic_samples)
         cfg.basic_seed = int(basic_seed) & 0xFFFFFFFF
         cfg.sample_rank, cfg.sample_world = int(sample_rank), int(sample_world)
+        if devices is not None and len(devices) == 1:
+            cfg.device_id = int(devices[0])
         if devices is not None and len(devices) > 1:
             cfg.n_devices = len(devices)
             for k, d in enumerate(devices):
@@ -147,8 +149,35 @@ class Renderer:
         self._ck(self._lib.pt_upload_env(self._h, _fp(h), ww, hh, None if c is None else _fp(c)), "pt_upload_env")
 
     def upload_shapes(self, shapes: np.ndarray):
-        s = np.ascontiguousarray(shapes, np.float32).reshape(-1, 24)
-        self._ck(self._lib.pt_upload_shapes(self._h, _fp(s), s.shape[0]), "pt_upload_shapes")
+        """BASIC: n x 24 f64 shape records (scenes.cornell_shapes, include/pt_scene.h)."""
+        s = np.ascontiguousarray(shapes, np.float64).reshape(-1, 24)
+        self._ck(self._lib.pt_upload_shapes(self._h, s.ctypes.data_as(_native.c_double_p), s.shape[0]),
+                 "pt_upload_shapes")
+
+    def basic_image(self) -> np.ndarray:
+        """BASIC: the reference's double image (h, w, 3), row 0 = top (BasicRayTracingWithC++/main.cpp:356)."""
+        out = np.empty((self.height, self.width, 3), np.float64)
+        self._ck(self._lib.pt_download_basic_image(self._h, out.ctypes.data_as(_native.c_double_p)),
+                 "pt_download_basic_image")
+        return out
+
+    def set_basic_stream(self, stream, offsets):
+        """BASIC: replay a recorded randf() stream; offsets (samples, h, w) = where each pixel sample's
+        draws start. stream None returns to the per-pixel counter RNG. Returns nothing."""
+        if stream is None:
+            self._ck(self._lib.pt_set_basic_stream(self._h, None, 0, None, 0), "pt_set_basic_stream")
+            return
+        st = np.ascontiguousarray(stream, np.float64).reshape(-1)
+        off = np.ascontiguousarray(offsets, np.int64).reshape(-1)
+        self._keep_stream = (st, off)
+        self._ck(self._lib.pt_set_basic_stream(self._h, st.ctypes.data_as(_native.c_double_p), st.size,
+                                               off.ctypes.data_as(C.POINTER(C.c_int64)), off.size),
+                 "pt_set_basic_stream")
+
+    def basic_replay_overruns(self) -> int:
+        c = C.c_int64()
+        self._ck(self._lib.pt_basic_replay_overruns(self._h, C.byref(c)), "pt_basic_replay_overruns")
+        return c.value
 
     def render_frame(self, eye, camera_rotate, frame_counter: int, download: bool = False, sync: bool = True):
         e = np.ascontiguousarray(eye, np.float32)

@@ -194,6 +194,15 @@ def write_png(path: str, img: np.ndarray, gamma: float = 2.2, flip_rows: bool = 
                   None, f"write_png({path})")
 
 
+def imshow_bytes(image: np.ndarray) -> np.ndarray:
+    """BasicRayTracingWithC++'s imshow conversion (main.cpp:183) of its double image:
+    (unsigned char)clamp(pow(v, 1.0f / 2.2f) * 255, 0.0, 255.0) -- the exponent is the float
+    1/2.2 promoted to double, the cast truncates. (h, w, 3) -> uint8, same row order."""
+    e = np.float64(np.float32(1.0) / np.float32(2.2))
+    v = np.power(np.asarray(image, np.float64)[..., :3], e) * 255.0
+    return np.clip(v, 0.0, 255.0).astype(np.uint8)
+
+
 def read_pfm(path: str) -> np.ndarray:
     """(h, w, 3) f32 in stored row order (PFM rows run bottom to top)."""
     with open(path, "rb") as f:

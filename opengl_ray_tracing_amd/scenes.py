@@ -217,27 +217,30 @@ def scene_c5() -> Scene:
 
 
 def cornell_shapes() -> np.ndarray:
-    """BasicRayTracingWithC++/main.cpp:306-353 as 24-float shape records (oracle/pt_oracle.h)."""
+    """BasicRayTracingWithC++/main.cpp:306-353 as 24-double shape records (include/pt_scene.h):
+    the vec3 fields hold the float values glm stores (vec3 of double literals rounds each to
+    float), the material rates and the sphere radius the reference's doubles (:49-59, :130)."""
     RED, GREEN, BLUE = (1, 0.5, 0.5), (0.5, 1, 0.5), (0.5, 0.5, 1)
     YELLOW, CYAN, WHITE = (1.0, 1.0, 0.1), (0.1, 1.0, 1.0), (1, 1, 1)
     recs = []
+    f32 = lambda v: np.asarray(v, np.float64).astype(np.float32).astype(np.float64)  # noqa: E731
 
     def mat(rec, color, emissive=False, spec=0.0, rough=1.0, refr=0.0, angle=1.0, rrough=0.0):
-        rec[10:13] = color
+        rec[10:13] = f32(color)
         rec[16] = 1.0 if emissive else 0.0
         rec[17], rec[18], rec[19], rec[20], rec[21] = spec, rough, refr, angle, rrough
 
     def sphere(o, r, c, **kw):
-        rec = np.zeros(24, np.float32)
+        rec = np.zeros(24, np.float64)
         rec[0] = 1.0
-        rec[1:4] = o
+        rec[1:4] = f32(o)
         rec[22] = r
         mat(rec, c, **kw)
         recs.append(rec)
 
     def tri(p1, p2, p3, c, **kw):
-        rec = np.zeros(24, np.float32)
-        p1, p2, p3 = (np.asarray(p, np.float32) for p in (p1, p2, p3))
+        rec = np.zeros(24, np.float64)
+        p1, p2, p3 = (np.asarray(p, np.float64).astype(np.float32) for p in (p1, p2, p3))
         rec[1:4], rec[4:7], rec[7:10] = p1, p2, p3
         e1, e2 = p2 - p1, p3 - p1
         # glm cross + normalize in f32, the reference's order (main.cpp:85)

@@ -690,26 +690,81 @@ static void shade_gl_pixel(Ctx* cx, const orc_frame* f, int px, int py, float* a
 }
 
 /* ---------------------------------------------------- BASIC (CPU tracer B) */
+/* The arithmetic is the reference binary's: glm vec3 is float, the Material
+ * rates, the sphere radius, HitResult::distance and the image are double
+ * (B:49-68, :130, :356), and every mixed expression is evaluated in the type
+ * C++ promotes it to. Pinned byte for byte against the reference compiled here
+ * (tests/golden/basic/, oracle/ref_basic.cpp; test_basic_serial_equals_reference). */
 typedef struct {
   int isHit;
-  float distance;
+  double distance;
   v3 hitPoint;
   v3 normal, color;
   int emissive;
-  float specularRate, roughness, refractRate, refractAngle, refractRoughness;
+  double specularRate, roughness, refractRate, refractAngle, refractRoughness;
 } BHit;
 
-static void bfill(BHit* r, const float* sh) {
-  r->color = V3(sh[10], sh[11], sh[12]);
-  r->emissive = sh[16] != 0.0f;
+/* The random stream. ORC_RNG_COUNTER: a per-pixel wang-hash stream (the
+ * parallel CPU baseline and the GPU kernel); ORC_RNG_MT19937: the reference's
+ * one global std::mt19937 read through uniform_real_distribution<double>
+ * (B:208-214), consumed in the reference's serial loop order. */
+typedef struct { uint32_t mt[624]; int idx; } Mt19937;
+static void mt_seed(Mt19937* m, uint32_t s) {
+  m->mt[0] = s;
+  for (int i = 1; i < 624; i++) m->mt[i] = 1812433253u * (m->mt[i - 1] ^ (m->mt[i - 1] >> 30)) + (uint32_t)i;
+  m->idx = 624;
+}
+static uint32_t mt_next(Mt19937* m) {
+  if (m->idx >= 624) {
+    for (int i = 0; i < 624; i++) {
+      uint32_t y = (m->mt[i] & 0x80000000u) | (m->mt[(i + 1) % 624] & 0x7fffffffu);
+      m->mt[i] = m->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    m->idx = 0;
+  }
+  uint32_t y = m->mt[m->idx++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+/* libstdc++ generate_canonical<double, 53> over a 32-bit engine: two draws,
+ * (g1 + g2 * 2^32) / 2^64 summed in double, 1.0 mapped to the largest double
+ * below it; uniform_real_distribution(0, 1) returns it unchanged (x * 1 + 0). */
+static double mt_canonical(Mt19937* m) {
+  double sum = (double)mt_next(m);
+  sum += (double)mt_next(m) * 4294967296.0;
+  double r = sum / 18446744073709551616.0;
+  if (r >= 1.0) r = nextafter(1.0, 0.0);
+  return r;
+}
+
+enum { ORC_RNG_COUNTER = 0, ORC_RNG_MT19937 = 1 };
+typedef struct {
+  int kind;
+  uint32_t seed;     /* counter */
+  Mt19937* mt;       /* mt19937 */
+  int64_t draws;     /* randf() calls so far (mt19937) */
+} BRng;
+/* randf B:211-214 */
+static double b_rand(BRng* g) {
+  if (g->kind == ORC_RNG_MT19937) { g->draws++; return mt_canonical(g->mt); }
+  return (double)wang(&g->seed) / 4294967296.0;
+}
+
+static void bfill(BHit* r, const double* sh) {
+  r->color = V3((float)sh[10], (float)sh[11], (float)sh[12]);
+  r->emissive = sh[16] != 0.0;
   r->specularRate = sh[17]; r->roughness = sh[18]; r->refractRate = sh[19];
   r->refractAngle = sh[20]; r->refractRoughness = sh[21];
 }
 /* Triangle::intersect B:90-122 */
-static BHit b_tri(const float* sh, v3 S, v3 d) {
+static BHit b_tri(const double* sh, v3 S, v3 d) {
   BHit res; memset(&res, 0, sizeof(res));
-  v3 p1 = V3(sh[1], sh[2], sh[3]), p2 = V3(sh[4], sh[5], sh[6]), p3 = V3(sh[7], sh[8], sh[9]);
-  v3 n = V3(sh[13], sh[14], sh[15]);
+  v3 p1 = V3((float)sh[1], (float)sh[2], (float)sh[3]), p2 = V3((float)sh[4], (float)sh[5], (float)sh[6]);
+  v3 p3 = V3((float)sh[7], (float)sh[8], (float)sh[9]);
+  v3 n = V3((float)sh[13], (float)sh[14], (float)sh[15]);
   v3 N = n;
   if (dot(N, d) > 0.0f) N = neg(N);
   if (fabsf(dot(N, d)) < 0.00001f) return res;
@@ -725,16 +780,20 @@ static BHit b_tri(const float* sh, v3 S, v3 d) {
   res.normal = N;
   return res;
 }
-/* Sphere::intersect B:135-164 (|SH| quirk kept) */
-static BHit b_sphere(const float* sh, v3 S, v3 d) {
+/* Sphere::intersect B:135-164: OS, SH, t are float (glm length / dot); pow(x, 2)
+ * of a float is exact in double; R is double, so OH > R and PH are double
+ * expressions (pow(R, 2) == R * R for the scene's radii, test_basic_sphere_pow);
+ * length(SH) of a float is |SH|. */
+static BHit b_sphere(const double* sh, v3 S, v3 d) {
   BHit res; memset(&res, 0, sizeof(res));
-  v3 O = V3(sh[1], sh[2], sh[3]);
-  float R = sh[22];
-  float OS = sqrtf(dot(sub(O, S), sub(O, S)));
-  float SH = dot(sub(O, S), d);
-  float OH = sqrtf(OS * OS - SH * SH);
-  if (OH > R) return res;
-  float PH = sqrtf(R * R - OH * OH);
+  v3 O = V3((float)sh[1], (float)sh[2], (float)sh[3]);
+  double R = sh[22];
+  v3 OSv = sub(O, S);
+  float OS = sqrtf(dot(OSv, OSv));
+  float SH = dot(OSv, d);
+  float OH = (float)sqrt((double)OS * (double)OS - (double)SH * (double)SH);
+  if ((double)OH > R) return res;
+  float PH = (float)sqrt(R * R - (double)OH * (double)OH);
   float t1 = fabsf(SH) - PH;
   float t2 = fabsf(SH) + PH;
   float t = (t1 < 0) ? t2 : t1;
@@ -745,103 +804,178 @@ static BHit b_sphere(const float* sh, v3 S, v3 d) {
   res.normal = normalize(sub(P, O));
   return res;
 }
-/* shoot B:192-205 */
+/* shoot B:192-205 (res.distance is a double initialised from 1145141919.810f) */
 static BHit b_shoot(Ctx* cx, v3 S, v3 d) {
   const orc_scene* s = cx->s;
   BHit res; memset(&res, 0, sizeof(res));
-  res.distance = 1145141919.810f;
+  res.distance = (double)1145141919.810f;
   cx->c.rays++;
   for (int k = 0; k < s->nShapes; k++) {
-    const float* sh = s->shapes + (size_t)k * ORC_SHAPE_FLOATS;
-    BHit r = (sh[0] == 1.0f) ? b_sphere(sh, S, d) : b_tri(sh, S, d);
+    const double* sh = s->shapes + (size_t)k * ORC_SHAPE_DOUBLES;
+    BHit r = (sh[0] == 1.0) ? b_sphere(sh, S, d) : b_tri(sh, S, d);
     if (r.isHit && r.distance < res.distance) res = r;
   }
   return res;
 }
-/* randomVec3 B:217-234 (args evaluated left to right here) / randomDirection B:237-250 */
-static v3 b_randomDirection(v3 n, uint32_t* seed) {
+/* randomVec3 B:217-234: vec3(randf(), randf(), randf()) -- the compiled reference
+ * evaluates the three arguments right to left (g++ and MSVC on x86-64), so z takes
+ * the first draw; 2.0f * v - vec3(1) in float, dot(d, d) > 1.0 in double.
+ * randomDirection B:237-250. */
+static v3 b_randomDirection(v3 n, BRng* g) {
   v3 d;
   do {
-    float a = randf(seed), b = randf(seed), c = randf(seed);
-    d = sub(scl(V3(a, b, c), 2.0f), V3(1, 1, 1));
-  } while (dot(d, d) > 1.0f);
+    double z = b_rand(g), y = b_rand(g), x = b_rand(g);
+    d = sub(scl(V3((float)x, (float)y, (float)z), 2.0f), V3(1, 1, 1));
+  } while ((double)dot(d, d) > 1.0);
   return normalize(add(normalize(d), n));
 }
-/* glm refract (include/glm/detail/func_geometric.inl:113-123) */
+/* glm reflect (func_geometric.inl:104-110): I - N * dot(N, I) * 2 */
+static v3 b_reflect(v3 I, v3 N) { return sub(I, scl(scl(N, dot(N, I)), 2.0f)); }
+/* glm refract (func_geometric.inl:113-123) */
 static v3 b_refract(v3 I, v3 N, float eta) {
   float dotValue = dot(N, I);
   float k = 1.0f - eta * eta * (1.0f - dotValue * dotValue);
-  if (k < 0.0f) return V3(0, 0, 0);
+  if (!(k >= 0.0f)) return V3(0, 0, 0);
   return sub(scl(I, eta), scl(N, eta * dotValue + sqrtf(k)));
 }
-/* One lobe choice + new direction, shared by the primary vertex (B:399-422)
- * and pathTracing (B:268-294). Returns the lobe: 0 specular, 1 refract, 2 diffuse. */
-static int b_lobe(const BHit* res, v3 din, uint32_t* seed, v3* dout) {
-  v3 rd = b_randomDirection(res->normal, seed);
-  float r = randf(seed);
+/* glm mix(vec3, vec3, double) (func_common.inl:103-111): computed in double, stored as float */
+static v3 b_mixd(v3 x, v3 y, double a) {
+  const double b = 1.0 - a;
+  return V3((float)((double)x.x * b + (double)y.x * a), (float)((double)x.y * b + (double)y.y * a),
+            (float)((double)x.z * b + (double)y.z * a));
+}
+/* One lobe choice + new direction, shared by the primary vertex (B:399-422) and
+ * pathTracing (B:268-294). Returns the lobe: 0 specular, 1 refract, 2 diffuse. */
+static int b_lobe(const BHit* res, v3 din, BRng* g, v3* dout) {
+  v3 rd = b_randomDirection(res->normal, g);
+  double r = b_rand(g);
   if (r < res->specularRate) {
-    v3 ref = normalize(reflect3(din, res->normal));
-    *dout = mixv(ref, rd, res->roughness);
+    v3 ref = normalize(b_reflect(din, res->normal));
+    *dout = b_mixd(ref, rd, res->roughness);
     return 0;
   } else if (res->specularRate <= r && r <= res->refractRate) {
-    v3 ref = normalize(b_refract(din, res->normal, res->refractAngle));
-    *dout = mixv(ref, neg(rd), res->refractRoughness);
+    v3 ref = normalize(b_refract(din, res->normal, (float)res->refractAngle));
+    *dout = b_mixd(ref, neg(rd), res->refractRoughness);
     return 1;
   }
   *dout = rd;
   return 2;
 }
-/* pathTracing B:252-297, recursion unrolled into a throughput product. */
-static v3 b_path(Ctx* cx, v3 S, v3 d, int maxDepth, uint32_t* seed) {
-  v3 thr = V3(1, 1, 1);
+#define ORC_BASIC_MAX_DEPTH 64
+/* pathTracing B:252-297 from depth 0. The recursion's products are formed on the
+ * way back up (color = pathTracing(depth + 1) * cosine [* srcColor], / P), so each
+ * vertex's factors are kept and folded from the deepest vertex upward. */
+static v3 b_path(Ctx* cx, v3 S, v3 d, int maxDepth, BRng* g) {
+  float cosv[ORC_BASIC_MAX_DEPTH + 1];
+  v3 col[ORC_BASIC_MAX_DEPTH + 1];
+  int diffuse[ORC_BASIC_MAX_DEPTH + 1];
+  const float P = 0.8f; /* B:264 float P = 0.8 */
+  v3 v = V3(0, 0, 0);
+  int n = 0;
+  if (maxDepth > ORC_BASIC_MAX_DEPTH) maxDepth = ORC_BASIC_MAX_DEPTH;
   for (int depth = 0;; depth++) {
-    if (depth > maxDepth) return V3(0, 0, 0);
+    if (depth > maxDepth) break;
     BHit res = b_shoot(cx, S, d);
-    if (!res.isHit) return V3(0, 0, 0);
-    if (res.emissive) return mul(thr, res.color);
-    float r = randf(seed);
-    const float P = 0.8f;
-    if (r > P) return V3(0, 0, 0);
+    if (!res.isHit) break;
+    if (res.emissive) { v = res.color; break; }
+    double r = b_rand(g);
+    if (r > (double)P) break;
     v3 nd;
-    float cosine = fabsf(dot(neg(d), res.normal));
-    int lobe = b_lobe(&res, d, seed, &nd);
-    thr = scl(thr, cosine);
-    if (lobe == 2) thr = mul(thr, res.color);
-    thr = sdiv(thr, P);
+    int lobe = b_lobe(&res, d, g, &nd);  /* randomDirection, then randf() (B:270, :276) */
+    cosv[n] = fabsf(dot(neg(d), res.normal));
+    col[n] = res.color;
+    diffuse[n] = lobe == 2;
+    n++;
     S = res.hitPoint;
     d = nd;
   }
+  for (int k = n - 1; k >= 0; k--) {
+    v = scl(v, cosv[k]);
+    if (diffuse[k]) v = mul(v, col[k]);
+    v = sdiv(v, P);
+  }
+  return v;
 }
-/* pixel loop body B:366-430, one sample k = frameCounter */
-static void shade_basic_pixel(Ctx* cx, const orc_frame* f, int j, int i, float* accum) {
-  const int W = f->width, H = f->height;
-  uint32_t k = sample_index(f);
-  uint32_t seed = ((uint32_t)j * 1973u + (uint32_t)i * 9277u + k * 26699u + f->basicSeed * 0x9E3779B9u) | 1u;
-  /* B:369-376: the screen coordinate is formed in double, then stored in a float vec3 */
+/* pixel loop body B:367-429 for pixel (j, i) of one sample: the value added to image */
+static v3 b_pixel(Ctx* cx, int j, int i, int W, int H, int maxDepth, float brightness, BRng* g) {
   double xd = 2.0 * (double)j / (double)W - 1.0;
   double yd = 2.0 * (double)(H - i) / (double)H - 1.0;
-  xd += (double)(randf(&seed) - 0.5f) / (double)W;
-  yd += (double)(randf(&seed) - 0.5f) / (double)H;
-  v3 coord = V3((float)xd, (float)yd, 1.1f);
+  xd += (b_rand(g) - 0.5) / (double)W;
+  yd += (b_rand(g) - 0.5) / (double)H;
+  v3 coord = V3((float)xd, (float)yd, (float)1.1);  /* SCREEN_Z B:27 is a double */
   v3 dir = normalize(sub(coord, V3(0, 0, 4.0f)));
   BHit res = b_shoot(cx, coord, dir);
   v3 color = V3(0, 0, 0);
-  int maxDepth = f->maxBounce >= 0 ? f->maxBounce : 8;
   if (res.isHit) {
     if (res.emissive) {
       color = res.color;
     } else {
       v3 nd;
-      int lobe = b_lobe(&res, dir, &seed, &nd);
-      v3 pt = b_path(cx, res.hitPoint, nd, maxDepth, &seed);
+      int lobe = b_lobe(&res, dir, g, &nd);
+      v3 pt = b_path(cx, res.hitPoint, nd, maxDepth, g);
       color = (lobe == 2) ? mul(pt, res.color) : pt;
-      /* BRIGHTNESS B:20 is a double, applied through glm's float scalar operator */
-      float brightness = (float)((double)(2.0f * 3.1415926f) * (1.0 / (double)f->basicSamples));
-      color = scl(color, brightness);
+      color = scl(color, brightness); /* color *= BRIGHTNESS: glm casts the double to float */
     }
   }
+  return color;
+}
+/* BRIGHTNESS B:20: (2.0f * 3.1415926f) * (1.0f / double(SAMPLE)), a double */
+static float b_brightness(int samples) { return (float)((double)(2.0f * 3.1415926f) * (1.0 / (double)samples)); }
+
+/* one sample of pixel (j, i) with the counter stream, added to the double image */
+static void shade_basic_pixel(Ctx* cx, const orc_frame* f, int j, int i, float* accum) {
+  const int W = f->width, H = f->height;
+  uint32_t k = sample_index(f);
+  BRng g;
+  memset(&g, 0, sizeof(g));
+  g.kind = ORC_RNG_COUNTER;
+  g.seed = ((uint32_t)j * 1973u + (uint32_t)i * 9277u + k * 26699u + f->basicSeed * 0x9E3779B9u) | 1u;
+  int maxDepth = f->maxBounce >= 0 ? f->maxBounce : 8;
+  v3 color = b_pixel(cx, j, i, W, H, maxDepth, b_brightness(f->basicSamples), &g);
+  double* im = f->basicImage + 3 * ((size_t)i * W + j);
+  if (f->frameCounter == 0) im[0] = im[1] = im[2] = 0.0;  /* sample 0 starts the image (B:356-357) */
+  im[0] += color.x; im[1] += color.y; im[2] += color.z;
   float* a = accum + 4 * ((size_t)i * W + j);
-  a[0] += color.x; a[1] += color.y; a[2] += color.z; a[3] = 1.0f;
+  a[0] = (float)im[0]; a[1] = (float)im[1]; a[2] = (float)im[2]; a[3] = 1.0f;
+}
+
+int orc_basic_serial(const orc_scene* s, int W, int H, int samples, uint32_t seed, int maxDepth, double* image,
+                     int64_t* offsets, int64_t* nDraws, orc_counters* counters) {
+  if (!s || !image || W <= 0 || H <= 0 || samples <= 0) return -1;
+  Mt19937* mt = (Mt19937*)malloc(sizeof(Mt19937));
+  if (!mt) return -3;
+  mt_seed(mt, seed);
+  Ctx cx;
+  cx.s = s;
+  memset(&cx.c, 0, sizeof(cx.c));
+  BRng g;
+  memset(&g, 0, sizeof(g));
+  g.kind = ORC_RNG_MT19937;
+  g.mt = mt;
+  const float br = b_brightness(samples);
+  memset(image, 0, sizeof(double) * (size_t)W * H * 3);
+  for (int k = 0; k < samples; k++)          /* B:361-432, serial as shipped (no /openmp) */
+    for (int i = 0; i < H; i++)
+      for (int j = 0; j < W; j++) {
+        if (offsets) offsets[((size_t)k * H + i) * W + j] = g.draws;
+        v3 c = b_pixel(&cx, j, i, W, H, maxDepth, br, &g);
+        double* p = image + 3 * ((size_t)i * W + j);
+        p[0] += c.x; p[1] += c.y; p[2] += c.z;
+      }
+  if (nDraws) *nDraws = g.draws;
+  if (counters) *counters = cx.c;
+  free(mt);
+  return 0;
+}
+
+int orc_mt_doubles(uint32_t seed, int64_t n, double* out) {
+  if (n < 0 || (n > 0 && !out)) return -1;
+  Mt19937* mt = (Mt19937*)malloc(sizeof(Mt19937));
+  if (!mt) return -3;
+  mt_seed(mt, seed);
+  for (int64_t k = 0; k < n; k++) out[k] = mt_canonical(mt);
+  free(mt);
+  return 0;
 }
 
 /* ------------------------------------------------------------ entry points */
@@ -849,6 +983,7 @@ int orc_render_pixels(const orc_scene* s, const orc_frame* f, const int* pix, in
                       float* accum, int nthreads, orc_counters* counters) {
   if (!s || !f || !accum) return -1;
   if (f->integrator != ORC_BASIC_CPU_COMPAT && (!s->tris || !s->nodes || s->nNodes < 2)) return -2;
+  if (f->integrator == ORC_BASIC_CPU_COMPAT && (!s->shapes || !f->basicImage)) return -2;
   long total = pix ? nPix : (long)f->width * f->height;
   orc_counters sum = {0, 0, 0, 0, 0};
 #ifdef _OPENMP

@@ -37,18 +37,19 @@ typedef struct orc_scene {
   const float* cache;  /* calculateHdrCache output, same dims (nullable) */
   int hdrW, hdrH;
   int hdrResolution;   /* uniform hdrResolution (IS main.cpp:853: = width) */
-  /* BASIC_CPU_COMPAT shape list (nShapes x ORC_SHAPE_FLOATS) */
-  const float* shapes;
+  /* BASIC_CPU_COMPAT shape list (nShapes x ORC_SHAPE_DOUBLES) */
+  const double* shapes;
   int nShapes;
 } orc_scene;
 
-/* BASIC shape record layout (floats) */
-#define ORC_SHAPE_FLOATS 24
+/* BASIC shape record layout (doubles; include/pt_scene.h PT_SHAPE_DOUBLES) */
+#define ORC_SHAPE_DOUBLES 24
 /* [0]=type (0 triangle, 1 sphere) [1..3]=p1 or sphere centre [4..6]=p2 [7..9]=p3
  * [10..12]=color [13..15]=normal (triangle: normalize(cross(p2-p1,p3-p1)))
  * [16]=isEmissive [17]=specularRate [18]=roughness [19]=refractRate
  * [20]=refractAngle [21]=refractRoughness [22]=sphere radius [23]=pad
- * (Material: BasicRayTracingWithC++/main.cpp:49-59; shapes :78-165) */
+ * The vec3 fields hold float values (glm vec3), the rates and the radius the
+ * reference's doubles (Material: BasicRayTracingWithC++/main.cpp:49-59; shapes :78-165) */
 
 typedef struct orc_frame {
   int width, height;
@@ -61,6 +62,8 @@ typedef struct orc_frame {
   uint32_t basicSeed;       /* BASIC: per-run seed of the counter RNG */
   int sampleRank, sampleWorld; /* RNG/Sobol sample = frameCounter*sampleWorld + sampleRank (0/0 = frameCounter);
                                   the running-mean weight stays 1/(frameCounter+1) (pt_abi.h pt_config) */
+  double* basicImage;       /* BASIC: the reference's double image (width x height x 3, B:356), summed in
+                               place (frameCounter 0 starts it); accum receives it as float */
 } orc_frame;
 
 typedef struct orc_counters {
@@ -79,6 +82,17 @@ typedef struct orc_counters {
  * pix == NULL renders every pixel. Returns 0 on success. */
 int orc_render_pixels(const orc_scene* s, const orc_frame* f, const int* pix, int nPix,
                       float* accum, int nthreads, orc_counters* counters);
+
+/* BasicRayTracingWithC++/main.cpp run as shipped: one global std::mt19937 seeded
+ * with `seed`, the sample / row / column loop B:361-432 serially. image: W x H x 3
+ * doubles (row 0 = top). offsets (nullable, samples x H x W): the stream position
+ * (number of randf() draws before) at which each pixel sample starts; *nDraws the
+ * total. This is what the reference binary computes, byte for byte
+ * (tests/golden/basic/, test_basic_serial_equals_reference). */
+int orc_basic_serial(const orc_scene* s, int W, int H, int samples, uint32_t seed, int maxDepth, double* image,
+                     int64_t* offsets, int64_t* nDraws, orc_counters* counters);
+/* The reference's randf() stream (B:208-214) from std::mt19937(seed): n doubles. */
+int orc_mt_doubles(uint32_t seed, int64_t n, double* out);
 
 /* Batch hitBVH (pass1.fsh:335-382): rays n x 6 (origin, direction). Miss: t = INF
  * (2147483648.f), tri = -1. brute != 0 uses hitArray over all triangles

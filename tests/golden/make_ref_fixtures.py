@@ -11,6 +11,11 @@ from /root/reference) and runs it on the inputs of tests/ref_scenes.py:
   ref/hdrcache_<env>.json      sha256 of calculateHdrCache's output for the
                                repository's decode of the shipped .hdr, and 4096
                                sampled texels of it
+  basic/ref_s<N>.json, .png    the reference CPU tracer (BasicRayTracingWithC++/main.cpp,
+                               oracle/ref_basic.cpp) at SAMPLE = N, std::mt19937 seeded
+                               5489: sha256 of its double image, 4096 sampled pixels
+                               of it, its 8-bit imshow bytes as a PNG, and their PSNR
+                               against the shipped 4000spp.png
 
     python tests/golden/make_ref_fixtures.py
 """
@@ -37,6 +42,7 @@ import ref_scenes  # noqa: E402
 from opengl_ray_tracing_amd import scenes  # noqa: E402
 
 OUT = Path(__file__).resolve().parent / "ref"
+BASIC = Path(__file__).resolve().parent / "basic"
 
 
 def sha(a: np.ndarray) -> str:
@@ -64,6 +70,28 @@ def run_scene(exe: Path, name: str, builder: str, tmp: Path):
     return tris, nodes
 
 
+def basic_fixtures(tmp: Path):
+    from PIL import Image
+    BASIC.mkdir(exist_ok=True)
+    ref4000 = np.asarray(Image.open(Path(__file__).resolve().parent / "4000spp.png"))[..., :3].astype(np.float64)
+    for n in ref_build.BASIC_SAMPLES:
+        fa, fb = tmp / f"b{n}.f64", tmp / f"b{n}.u8"
+        subprocess.run([str(ref_build.basic_exe(n)), str(fa), str(fb)], check=True)
+        img = np.fromfile(fa, np.float64).reshape(256, 256, 3)
+        u8 = np.fromfile(fb, np.uint8).reshape(256, 256, 3)
+        Image.fromarray(u8).save(BASIC / f"ref_s{n}.png")
+        rng = np.random.default_rng(5)
+        idx = rng.choice(256 * 256, 4096, replace=False)
+        psnr = 10 * np.log10(255.0 ** 2 / np.mean((u8.astype(np.float64) - ref4000) ** 2))
+        ent = {"samples": n, "seed": 5489, "width": 256, "height": 256,
+               "generator": "oracle/ref_basic.cpp (BasicRayTracingWithC++/main.cpp compiled from its source)",
+               "image_f64_sha256": sha(img), "image_u8_sha256": sha(u8), "png": f"ref_s{n}.png",
+               "sample_index": idx.tolist(), "sample_values": img.reshape(-1, 3)[idx].tolist(),
+               "channel_sums": img.reshape(-1, 3).sum(0).tolist(), "psnr_vs_4000spp_db": float(psnr)}
+        (BASIC / f"ref_s{n}.json").write_text(json.dumps(ent) + "\n")
+        print("basic", n, round(psnr, 3))
+
+
 def main():
     exe = ref_build.build()
     if exe is None:
@@ -71,6 +99,8 @@ def main():
     OUT.mkdir(exist_ok=True)
     with tempfile.TemporaryDirectory() as d:
         tmp = Path(d)
+        if len(sys.argv) == 1 or "basic" in sys.argv[1:]:
+            basic_fixtures(tmp)
         for name, builder in ref_scenes.BUILDS:
             if len(sys.argv) > 1 and name not in sys.argv[1:]:
                 continue

@@ -16,19 +16,20 @@ ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = ROOT / "oracle" / "liboracle.so"
 
 c_float_p = C.POINTER(C.c_float)
+c_double_p = C.POINTER(C.c_double)
 
 
 class OrcScene(C.Structure):
     _fields_ = [("tris", c_float_p), ("nTriangles", C.c_int), ("nodes", c_float_p), ("nNodes", C.c_int),
                 ("hdr", c_float_p), ("cache", c_float_p), ("hdrW", C.c_int), ("hdrH", C.c_int),
-                ("hdrResolution", C.c_int), ("shapes", c_float_p), ("nShapes", C.c_int)]
+                ("hdrResolution", C.c_int), ("shapes", c_double_p), ("nShapes", C.c_int)]
 
 
 class OrcFrame(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("integrator", C.c_int), ("maxBounce", C.c_int),
                 ("frameCounter", C.c_uint32), ("eye", C.c_float * 3), ("cameraRotate", C.c_float * 16),
                 ("basicSamples", C.c_int), ("basicSeed", C.c_uint32), ("sampleRank", C.c_int),
-                ("sampleWorld", C.c_int)]
+                ("sampleWorld", C.c_int), ("basicImage", c_double_p)]
 
 
 class OrcCounters(C.Structure):
@@ -74,6 +75,12 @@ def load():
         lib.orc_pixel_rng.restype = None
         lib.orc_hdr_cache.argtypes = [c_float_p, C.c_int, C.c_int, c_float_p]
         lib.orc_hdr_cache.restype = C.c_int
+        lib.orc_basic_serial.argtypes = [C.POINTER(OrcScene), C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_int,
+                                         c_double_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                         C.POINTER(OrcCounters)]
+        lib.orc_basic_serial.restype = C.c_int
+        lib.orc_mt_doubles.argtypes = [C.c_uint32, C.c_int64, c_double_p]
+        lib.orc_mt_doubles.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -106,8 +113,11 @@ class Oracle:
                 cache = hdr_cache(hdr)
             s.hdr, s.cache, s.hdrW, s.hdrH, s.hdrResolution = fp(hdr), fp(cache), w, h, w
         if shapes is not None:
-            s.shapes, s.nShapes = fp(shapes), int(np.asarray(shapes).reshape(-1, 24).shape[0])
+            sh = np.ascontiguousarray(shapes, np.float64).reshape(-1, 24)
+            self._keep.append(sh)
+            s.shapes, s.nShapes = sh.ctypes.data_as(c_double_p), int(sh.shape[0])
         self.scene = s
+        self.basic_image = None  # BASIC: the reference's double image, summed across frames
 
     def render(self, width, height, integrator, frame, eye=None, rot=None, accum=None, pixels=None,
                max_bounce=-1, threads=8, basic_samples=128, basic_seed=0, sample_rank=0, sample_world=1):
@@ -126,6 +136,10 @@ class Oracle:
         if accum is None:
             accum = np.zeros((height, width, 4), np.float32)
         assert accum.dtype == np.float32 and accum.flags.c_contiguous and accum.shape == (height, width, 4)
+        if f.integrator == INTEG["basic"]:
+            if self.basic_image is None or self.basic_image.shape != (height, width, 3):
+                self.basic_image = np.zeros((height, width, 3), np.float64)
+            f.basicImage = self.basic_image.ctypes.data_as(c_double_p)
         cnt = OrcCounters()
         if pixels is not None:
             px = np.ascontiguousarray(pixels, np.int32).reshape(-1, 2)
@@ -136,6 +150,20 @@ class Oracle:
                                         threads, C.byref(cnt))
         assert rc == 0, rc
         return accum, Counters(cnt.rays, cnt.nodes, cnt.tris, cnt.mats, cnt.texels)
+
+    def basic_serial(self, width=256, height=256, samples=4, seed=5489, max_depth=8, offsets=False):
+        """BasicRayTracingWithC++/main.cpp as shipped (one mt19937 stream, serial loop):
+        -> (image (h, w, 3) float64, row 0 = top, offsets (samples, h, w) int64 or None, draws, Counters)"""
+        img = np.zeros((height, width, 3), np.float64)
+        off = np.zeros((samples, height, width), np.int64) if offsets else None
+        nd = C.c_int64()
+        cnt = OrcCounters()
+        rc = self.lib.orc_basic_serial(C.byref(self.scene), width, height, samples, seed & 0xFFFFFFFF, max_depth,
+                                       img.ctypes.data_as(c_double_p),
+                                       None if off is None else off.ctypes.data_as(C.POINTER(C.c_int64)),
+                                       C.byref(nd), C.byref(cnt))
+        assert rc == 0, rc
+        return img, off, nd.value, Counters(cnt.rays, cnt.nodes, cnt.tris, cnt.mats, cnt.texels)
 
     def trace_closest(self, rays, brute=False):
         r = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
@@ -161,6 +189,13 @@ def sobol(d: int, i: int) -> float:
 def pixel_rng(px, py, frame, n):
     out = np.empty(n, np.float32)
     load().orc_pixel_rng(px, py, frame, n, out.ctypes.data_as(c_float_p))
+    return out
+
+
+def mt_doubles(seed: int, n: int) -> np.ndarray:
+    """The reference's randf() stream (BasicRayTracingWithC++/main.cpp:208-214) from std::mt19937(seed)."""
+    out = np.empty(n, np.float64)
+    assert load().orc_mt_doubles(seed & 0xFFFFFFFF, n, out.ctypes.data_as(c_double_p)) == 0
     return out
 
 

@@ -49,6 +49,8 @@ def test_fmath_device_equals_host(fn):
 
 
 def test_basic_integrator_matches_oracle():
+    """Counter-RNG mode: the double image and its f32 copy bit for bit against the oracle,
+    which shares its arithmetic with the reference-pinned serial mode (test_basic_ref)."""
     sh = scenes.cornell_shapes()
     w = h = 256
     with Renderer(w, h, "basic", basic_samples=4) as r:
@@ -56,6 +58,7 @@ def test_basic_integrator_matches_oracle():
         for k in range(4):
             r.render_frame(np.zeros(3, np.float32), np.eye(4, dtype=np.float32), k)
         g = r.accum()
+        gimg = r.basic_image()
         st = r.stats()
     o = oracle.Oracle(shapes=sh)
     acc = np.zeros((h, w, 4), np.float32)
@@ -64,9 +67,41 @@ def test_basic_integrator_matches_oracle():
         acc, c = o.render(w, h, "basic", k, accum=acc, basic_samples=4)
         rays += c.rays
     s = parity.assert_parity(g.reshape(-1, 4), acc.reshape(-1, 4), "basic")
-    print("basic", s)
-    assert s["exact"] > 0.999
-    assert abs(int(st.rays) - rays) <= 1e-3 * rays
+    print("basic", s, "image bit-exact", np.array_equal(gimg, o.basic_image))
+    assert np.array_equal(gimg.view(np.uint64), o.basic_image.view(np.uint64))
+    assert np.array_equal(g.view(np.uint32), acc.view(np.uint32))
+    assert int(st.rays) == rays
+
+
+def test_basic_replay_equals_reference_image():
+    """The GPU kernel replaying the reference's random stream (std::mt19937 seeded 5489, the
+    draws of each pixel sample located by a serial pass of the checker) renders the reference
+    CPU tracer's own image: its double image bit for bit (sha256 of tests/golden/basic/ref_s4,
+    made by BasicRayTracingWithC++/main.cpp compiled from source) and its 8-bit output."""
+    import hashlib
+    import json
+    from pathlib import Path
+
+    from opengl_ray_tracing_amd.scene import imshow_bytes
+    ref = json.loads((Path(__file__).resolve().parent / "golden" / "basic" / "ref_s4.json").read_text())
+    sh = scenes.cornell_shapes()
+    o = oracle.Oracle(shapes=sh)
+    _, off, draws, c = o.basic_serial(samples=4, seed=ref["seed"], offsets=True)  # where each sample's draws start
+    stream = oracle.mt_doubles(ref["seed"], draws)
+    with Renderer(256, 256, "basic", basic_samples=4) as r:
+        r.upload_shapes(sh)
+        r.set_basic_stream(stream, off)
+        for k in range(4):
+            r.render_frame(np.zeros(3, np.float32), np.eye(4, dtype=np.float32), k)
+        img = r.basic_image()
+        over = r.basic_replay_overruns()
+        st = r.stats()
+    assert over == 0
+    got = img.reshape(-1, 3)[ref["sample_index"]]
+    print("replay: sampled pixels equal", np.array_equal(got, np.asarray(ref["sample_values"])))
+    assert hashlib.sha256(img.tobytes()).hexdigest() == ref["image_f64_sha256"]
+    assert hashlib.sha256(imshow_bytes(img).tobytes()).hexdigest() == ref["image_u8_sha256"]
+    assert int(st.rays) == c.rays == 914124
 
 
 @pytest.mark.parametrize("world", [2, 4])

@@ -50,8 +50,11 @@ def main():
         st = r.stats()
         if a.out.endswith(".pfm"):
             write_pfm(a.out, r.accum())
-        elif basic:
-            write_png(a.out, r.accum(), 2.2, flip_rows=False)
+        elif basic:  # imshow of the reference's double image (main.cpp:169-190)
+            from PIL import Image
+
+            from opengl_ray_tracing_amd.scene import imshow_bytes
+            Image.fromarray(imshow_bytes(r.basic_image())).save(a.out)
         else:
             write_png(a.out, r.tonemap(1.5), 2.2, flip_rows=True)
     print(f"{a.config}: {a.frames} frames in {dt * 1e3:.1f} ms, {st.rays / dt / 1e6:.1f} Mrays/s -> {a.out}")
