@@ -1090,3 +1090,76 @@ int orc_hdr_cache(const float* HDR, int width, int height, float* cache) {
   free(pdf); free(margin); free(cdfx); free(cdfy);
   return 0;
 }
+
+/* ------------------------------------------------- per-function parity hooks */
+/* Function fn of this restatement on n inputs, in the layout of the reference
+ * shader harness's ref_glsl_fn (oracle/ref_glsl.cpp: the pass1.fsh text compiled
+ * as C++), so tests/test_glsl_ref.py can compare them on random inputs. Each case
+ * calls the function the integrators call, composed as the integrators compose it. */
+static inline uint32_t o_ubits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float o_fbits(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline v3 o_v3(const float* p) { return V3(p[0], p[1], p[2]); }
+static inline void o_put3(float* o, v3 v) { o[0] = v.x; o[1] = v.y; o[2] = v.z; }
+static Material o_mat(const float* p) {
+  Material m;
+  m.emissive = o_v3(p); m.baseColor = o_v3(p + 3);
+  m.subsurface = p[6]; m.metallic = p[7]; m.specular = p[8]; m.specularTint = p[9];
+  m.roughness = p[10]; m.anisotropic = p[11]; m.sheen = p[12]; m.sheenTint = p[13];
+  m.clearcoat = p[14]; m.clearcoatGloss = p[15]; m.IOR = p[16]; m.transmission = p[17];
+  return m;
+}
+static const int O_FN_IN[] = {1, 2, 2, 6, 6, 3, 24, 12, 1, 2, 2, 5, 2, 5, 33, 33, 27, 27, 5, 9, 9, 26, 3, 2, 1};
+static const int O_FN_OUT[] = {2, 1, 2, 2, 3, 6, 9, 1, 1, 1, 1, 1, 1, 1, 3, 3, 3, 1, 3, 3, 3, 3, 2, 1, 4};
+
+int orc_glsl_fn(int fn, const float* in, float* out, int n) {
+  if (fn < 0 || fn >= (int)(sizeof(O_FN_IN) / sizeof(O_FN_IN[0])) || n < 0) return -1;
+  for (int k = 0; k < n; k++) {
+    const float* a = in + (size_t)k * O_FN_IN[fn];
+    float* o = out + (size_t)k * O_FN_OUT[fn];
+    switch (fn) {
+      case 0: { uint32_t sd = o_ubits(a[0]); uint32_t r = wang(&sd); o[0] = o_fbits(r); o[1] = o_fbits(sd); break; }
+      case 1: o[0] = sobolf(o_ubits(a[0]), o_ubits(a[1])); break;
+      case 2: {  /* sobolVec2(frameCounter + 1, bounce) as pt_mis forms it */
+        uint32_t gi = grayCode(o_ubits(a[0]));
+        uint32_t b = o_ubits(a[1]);
+        o[0] = sobolf(2u * b, gi);
+        o[1] = sobolf(2u * b + 1u, gi);
+        break;
+      }
+      case 3: { float u = a[4], v = a[5]; cranley_patterson((int)a[0], (int)a[1], &u, &v); o[0] = u; o[1] = v; break; }
+      case 4: o_put3(o, toNormalHemisphere(o_v3(a), o_v3(a + 3))); break;
+      case 5: { v3 t, b; getTangent(o_v3(a), &t, &b); o_put3(o, t); o_put3(o + 3, b); break; }
+      case 6: {
+        Tri t;
+        t.p1 = o_v3(a); t.p2 = o_v3(a + 3); t.p3 = o_v3(a + 6);
+        t.n1 = o_v3(a + 9); t.n2 = o_v3(a + 12); t.n3 = o_v3(a + 15);
+        Hit h = hitTriangle(t, o_v3(a + 18), o_v3(a + 21));
+        o[0] = h.isHit ? 1.0f : 0.0f; o[1] = h.isInside ? 1.0f : 0.0f; o[2] = h.distance;
+        o_put3(o + 3, h.isHit ? h.hitPoint : V3(0, 0, 0)); o_put3(o + 6, h.isHit ? h.normal : V3(0, 0, 0));
+        break;
+      }
+      case 7: o[0] = hitAABB(o_v3(a), o_v3(a + 3), o_v3(a + 6), o_v3(a + 9)); break;
+      case 8: o[0] = SchlickFresnel(a[0]); break;
+      case 9: o[0] = GTR1(a[0], a[1]); break;
+      case 10: o[0] = GTR2(a[0], a[1]); break;
+      case 11: o[0] = GTR2_aniso(a[0], a[1], a[2], a[3], a[4]); break;
+      case 12: o[0] = smithG_GGX(a[0], a[1]); break;
+      case 13: o[0] = smithG_GGX_aniso(a[0], a[1], a[2], a[3], a[4]); break;
+      case 14: case 15: {
+        Material m = o_mat(a + 15);
+        o_put3(o, BRDF_Evaluate_aniso(o_v3(a), o_v3(a + 3), o_v3(a + 6), o_v3(a + 9), o_v3(a + 12), &m));
+        break;
+      }
+      case 16: { Material m = o_mat(a + 9); o_put3(o, BRDF_Evaluate(o_v3(a), o_v3(a + 3), o_v3(a + 6), &m)); break; }
+      case 17: { Material m = o_mat(a + 9); o[0] = BRDF_Pdf(o_v3(a), o_v3(a + 3), o_v3(a + 6), &m); break; }
+      case 18: o_put3(o, SampleCosineHemisphere(a[0], a[1], o_v3(a + 2))); break;
+      case 19: o_put3(o, SampleGTR2(a[0], a[1], o_v3(a + 2), o_v3(a + 5), a[8])); break;
+      case 20: o_put3(o, SampleGTR1(a[0], a[1], o_v3(a + 2), o_v3(a + 5), a[8])); break;
+      case 21: { Material m = o_mat(a + 8); o_put3(o, SampleBRDF(a[0], a[1], a[2], o_v3(a + 3), o_v3(a + 6), &m)); break; }
+      case 22: { float u, w; toSpherical(o_v3(a), &u, &w); o[0] = u; o[1] = w; break; }
+      case 23: o[0] = misMixWeight(a[0], a[1]); break;
+      case 24: { uint32_t sd = o_ubits(a[0]); o_put3(o, SampleHemisphereRand(&sd)); o[3] = o_fbits(sd); break; }
+    }
+  }
+  return 0;
+}

@@ -105,6 +105,10 @@ uint32_t orc_wang_hash(uint32_t seed);
 float orc_sobol(uint32_t d, uint32_t i);
 void orc_pixel_rng(int px, int py, uint32_t frameCounter, int n, float* out);
 
+/* Per-function parity hook: function fn (0..24, the layout of oracle/ref_glsl.cpp
+ * ref_glsl_fn) on n inputs. */
+int orc_glsl_fn(int fn, const float* in, float* out, int n);
+
 /* calculateHdrCache restatement (IS main.cpp:555-652): cache_out w*h*3. */
 int orc_hdr_cache(const float* hdr, int w, int h, float* cache_out);
 

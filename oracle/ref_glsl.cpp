@@ -42,8 +42,17 @@
 #include <cstring>
 #include <utility>
 
+// glm enables its swizzle operators (pix.xy as a member) only with MS language
+// extensions or x86 intrinsics; the former changes no arithmetic (glm/detail/setup.hpp:75)
 #define GLM_FORCE_SWIZZLE
+#ifndef _MSC_EXTENSIONS
+#define _MSC_EXTENSIONS
+#define PT_UNDEF_MSC_EXTENSIONS
+#endif
 #include <glm/glm.hpp>
+#ifdef PT_UNDEF_MSC_EXTENSIONS
+#undef _MSC_EXTENSIONS
+#endif
 
 #include "pt_fmath.h"
 
@@ -229,6 +238,125 @@ int ref_glsl_render(int which, const ref_scene* s, int W, int H, const float eye
     else { PassIS f(u); f.main(); c = f.gl_FragData[0]; }
     float* o = accum_out + 4 * ((size_t)py * W + px);
     o[0] = c.x; o[1] = c.y; o[2] = c.z; o[3] = c.w;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- per-function
+// Function fn of the compiled shader text on n inputs (fixed strides, tests/test_glsl_ref.py
+// FUNCS; the oracle's orc_glsl_fn takes the same layout). Unsigned ints travel as float bits.
+// Member functions are called on one fragment object whose uniforms the input sets
+// (CranleyPatterson reads pix / width / height).
+static inline uint32_t ubits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+static inline float fbits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+static inline vec3 v3at(const float* p) { return vec3(p[0], p[1], p[2]); }
+static inline void put3(float* o, vec3 v) { o[0] = v.x; o[1] = v.y; o[2] = v.z; }
+}  // extern "C"
+template <class M>
+static M matAt(const float* p) {
+  M m;
+  m.emissive = v3at(p);
+  m.baseColor = v3at(p + 3);
+  m.subsurface = p[6]; m.metallic = p[7]; m.specular = p[8]; m.specularTint = p[9];
+  m.roughness = p[10]; m.anisotropic = p[11]; m.sheen = p[12]; m.sheenTint = p[13];
+  m.clearcoat = p[14]; m.clearcoatGloss = p[15]; m.IOR = p[16]; m.transmission = p[17];
+  return m;
+}
+extern "C" {
+
+static const int FN_IN[] = {1, 2, 2, 6, 6, 3, 24, 12, 1, 2, 2, 5, 2, 5, 33, 33, 27, 27, 5, 9, 9, 26, 3, 2, 1};
+static const int FN_OUT[] = {2, 1, 2, 2, 3, 6, 9, 1, 1, 1, 1, 1, 1, 1, 3, 3, 3, 1, 3, 3, 3, 3, 2, 1, 4};
+#define REF_NFN ((int)(sizeof(FN_IN) / sizeof(FN_IN[0])))
+
+int ref_glsl_fn_arity(int fn, int* nin, int* nout) {
+  if (fn < 0 || fn >= REF_NFN) return -1;
+  *nin = FN_IN[fn];
+  *nout = FN_OUT[fn];
+  return 0;
+}
+
+int ref_glsl_fn(int fn, const float* in, float* out, int n) {
+  if (fn < 0 || fn >= REF_NFN || n < 0) return -1;
+  if (ref_glsl_selfcheck() != 0) return -2;
+  Uniforms u{};
+  u.width = u.height = 1;
+  for (int k = 0; k < n; k++) {
+    const float* a = in + (size_t)k * FN_IN[fn];
+    float* o = out + (size_t)k * FN_OUT[fn];
+    PassIS is(u);
+    PassD d(u);
+    switch (fn) {
+      case 0: {  // wang_hash IS:78-85
+        uint32_t sd = ubits(a[0]);
+        uint32_t r = is.wang_hash(sd);
+        o[0] = fbits(r); o[1] = fbits(sd);
+        break;
+      }
+      case 1: o[0] = is.sobol(ubits(a[0]), ubits(a[1])); break;  // IS:101-109
+      case 2: { vec2 v = is.sobolVec2(ubits(a[0]), ubits(a[1])); o[0] = v.x; o[1] = v.y; break; }  // IS:112-116
+      case 3: {  // CranleyPatterson IS:118-136: pix of pixel (a0, a1) in an a2 x a3 frame
+        Uniforms w = u;
+        w.width = (int)a[2];
+        w.height = (int)a[3];
+        w.pix = vec3((float)(2 * (int)a[0] + 1) / (float)w.width - 1.0f, (float)(2 * (int)a[1] + 1) / (float)w.height - 1.0f, 0.0f);
+        PassIS f(w);
+        vec2 r = f.CranleyPattersonRotation(vec2(a[4], a[5]));
+        o[0] = r.x; o[1] = r.y;
+        break;
+      }
+      case 4: put3(o, is.toNormalHemisphere(v3at(a), v3at(a + 3))); break;  // IS:153-159
+      case 5: { vec3 t(0), b(0); is.getTangent(v3at(a), t, b); put3(o, t); put3(o + 3, b); break; }  // IS:161-172
+      case 6: {  // hitTriangle IS:251-301
+        PassIS::Triangle t;
+        t.p1 = v3at(a); t.p2 = v3at(a + 3); t.p3 = v3at(a + 6);
+        t.n1 = v3at(a + 9); t.n2 = v3at(a + 12); t.n3 = v3at(a + 15);
+        PassIS::Ray r;
+        r.startPosition = v3at(a + 18);
+        r.direction = v3at(a + 21);
+        PassIS::HitResult h = is.hitTriangle(t, r);
+        o[0] = h.isHit ? 1.0f : 0.0f; o[1] = h.isInside ? 1.0f : 0.0f; o[2] = h.distance;
+        put3(o + 3, h.isHit ? h.hitPoint : vec3(0)); put3(o + 6, h.isHit ? h.normal : vec3(0));
+        break;
+      }
+      case 7: {  // hitAABB IS:303-316
+        PassIS::Ray r;
+        r.startPosition = v3at(a);
+        r.direction = v3at(a + 3);
+        o[0] = is.hitAABB(r, v3at(a + 6), v3at(a + 9));
+        break;
+      }
+      case 8: o[0] = is.SchlickFresnel(a[0]); break;              // IS:390-394
+      case 9: o[0] = is.GTR1(a[0], a[1]); break;                   // IS:396-401
+      case 10: o[0] = is.GTR2(a[0], a[1]); break;                  // IS:403-407
+      case 11: o[0] = is.GTR2_aniso(a[0], a[1], a[2], a[3], a[4]); break;  // IS:409-411
+      case 12: o[0] = is.smithG_GGX(a[0], a[1]); break;            // IS:413-417
+      case 13: o[0] = is.smithG_GGX_aniso(a[0], a[1], a[2], a[3], a[4]); break;  // IS:419-421
+      case 14:  // BRDF_Evaluate_aniso IS:423-482
+        put3(o, is.BRDF_Evaluate_aniso(v3at(a), v3at(a + 3), v3at(a + 6), v3at(a + 9), v3at(a + 12),
+                                       matAt<PassIS::Material>(a + 15)));
+        break;
+      case 15:  // BRDF_Evaluate D:381-440 (the DisneyBRDF kernel's own text)
+        put3(o, d.BRDF_Evaluate(v3at(a), v3at(a + 3), v3at(a + 6), v3at(a + 9), v3at(a + 12),
+                                matAt<PassD::Material>(a + 15)));
+        break;
+      case 16: put3(o, is.BRDF_Evaluate(v3at(a), v3at(a + 3), v3at(a + 6), matAt<PassIS::Material>(a + 9))); break;  // IS:587-636
+      case 17: o[0] = is.BRDF_Pdf(v3at(a), v3at(a + 3), v3at(a + 6), matAt<PassIS::Material>(a + 9)); break;  // IS:669-706
+      case 18: put3(o, is.SampleCosineHemisphere(a[0], a[1], v3at(a + 2))); break;  // IS:485-496
+      case 19: put3(o, is.SampleGTR2(a[0], a[1], v3at(a + 2), v3at(a + 5), a[8])); break;  // IS:499-516
+      case 20: put3(o, is.SampleGTR1(a[0], a[1], v3at(a + 2), v3at(a + 5), a[8])); break;  // IS:519-536
+      case 21:  // SampleBRDF IS:539-570
+        put3(o, is.SampleBRDF(a[0], a[1], a[2], v3at(a + 3), v3at(a + 6), matAt<PassIS::Material>(a + 8)));
+        break;
+      case 22: { vec2 v = is.toSphericalCoord(v3at(a)); o[0] = v.x; o[1] = v.y; break; }  // IS:638-644
+      case 23: o[0] = is.misMixWeight(a[0], a[1]); break;  // IS:708-711
+      case 24: {  // SampleHemisphere() D:90-95 (z = rand(), then phi), from seed a0
+        d.seed = ubits(a[0]);
+        vec3 v = d.SampleHemisphere();
+        put3(o, v);
+        o[3] = fbits(d.seed);
+        break;
+      }
+    }
   }
   return 0;
 }

@@ -81,6 +81,8 @@ def load():
         lib.orc_basic_serial.restype = C.c_int
         lib.orc_mt_doubles.argtypes = [C.c_uint32, C.c_int64, c_double_p]
         lib.orc_mt_doubles.restype = C.c_int
+        lib.orc_glsl_fn.argtypes = [C.c_int, c_float_p, c_float_p, C.c_int]
+        lib.orc_glsl_fn.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -196,6 +198,14 @@ def mt_doubles(seed: int, n: int) -> np.ndarray:
     """The reference's randf() stream (BasicRayTracingWithC++/main.cpp:208-214) from std::mt19937(seed)."""
     out = np.empty(n, np.float64)
     assert load().orc_mt_doubles(seed & 0xFFFFFFFF, n, out.ctypes.data_as(c_double_p)) == 0
+    return out
+
+
+def glsl_fn(fn: int, x: np.ndarray, n_out: int) -> np.ndarray:
+    """The restatement's function fn (orc_glsl_fn, the layout of tests/ref_glsl.py FUNCS) on rows of x."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros((x.shape[0], n_out), np.float32)
+    assert load().orc_glsl_fn(fn, x.ctypes.data_as(c_float_p), out.ctypes.data_as(c_float_p), x.shape[0]) == 0
     return out
 
 
