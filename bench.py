@@ -42,13 +42,17 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+# hardware queues for the renderer's frames in flight (one stream each, pt_runtime.cpp depthStep),
+# set before torch or the renderer first initialises HIP (HIP's default is 4)
+if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 12:
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # VALU issue: 1024 SIMD-32s (256 CUs x 4) each issue one wave64 VALU instruction per 2 cycles
 # at the 2.4 GHz maximum clock (MI355X_MICROARCH.md "Wave scheduling"): 1228.8 G wave-instructions/s
 VALU_PEAK_GINST = 1024 * 2.4 / 2 * 1e9 / 1e9
 METRIC = "Mrays/sec + ms/frame (1 spp, 1080p) at 1/2/4/8 MI355X; CPU-ref spp-matched PSNR"
-PROBE_FRAMES = 20  # frames after a restart during which the renderer measures its tree and split policies
+PROBE_FRAMES = 90  # frames after a restart during which the renderer measures its policies (tree, split, order, depth)
 
 
 def parse():

@@ -66,7 +66,7 @@ static_assert((NUM_QUEUES & (NUM_QUEUES - 1)) == 0 && NUM_QUEUES <= 64, "NUM_QUE
 constexpr int RAY_SHARDS = 64;     // sharded ray counters (u64, one per 256-byte line)
 constexpr int RAY_SHARD_STRIDE = CTL_LINE_INTS / 2;  // in u64
 // control block layout (bytes)
-constexpr int MAX_SLOTS = 4;  // frames in flight the control block has queue counters for (pt_runtime.cpp PIPE)
+constexpr int MAX_SLOTS = 16;  // frames in flight the control block has queue counters for (pt_runtime.cpp PIPE)
 constexpr size_t CTL_QUEUES = 0;  // MAX_SLOTS x NUM_QUEUES padded int counters
 constexpr size_t CTL_STATS = (size_t)MAX_SLOTS * 64 * 256;            // 5 u64 cumulative fetch counters
 constexpr size_t CTL_RAYS = CTL_STATS + 256;                          // RAY_SHARDS padded u64 counters

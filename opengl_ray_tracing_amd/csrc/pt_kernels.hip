@@ -18,6 +18,8 @@
 //    instead of the reference's three); triangles as 64-byte records with the
 //    precomputed unit normal and plane offset.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include "pt_device.h"
@@ -1169,7 +1171,12 @@ hipError_t launchPack(const PackParams& p, const float4* accum, float* packed, h
 }
 hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s) {
   if (p.count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, col, frameCounter);
+  static const int bs = [] {
+    const char* e = std::getenv("PT_MIX_BLOCK");
+    const int v = e ? std::atoi(e) : 256;
+    return v == 64 || v == 128 || v == 256 || v == 512 || v == 1024 ? v : 256;
+  }();
+  hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + bs - 1) / bs)), dim3(bs), 0, s, p, accum, col, frameCounter);
   return hipGetLastError();
 }
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s) {

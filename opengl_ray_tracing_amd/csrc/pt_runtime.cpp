@@ -29,17 +29,29 @@
 using namespace pt;
 
 static constexpr int EV_RING = 64;
-// Frames in flight: the default megakernel's frame f runs on slot stream f % PIPE
-// with its own work queues, overflow stack, tile order and colour buffer, so
-// frame f+1 can fill the SIMDs that frame f's last long paths leave idle. Each
-// frame's running-mean update (mixKernel) waits for the previous frame's, so the
-// accumulation is updated in frame order and the image is bit for bit the one
-// of serial frames (c4: two overlapped frames measured 1.57x the throughput of
-// serial ones, tools/overlap_probe.py).
+// Frames in flight: the default megakernel's frame g (its pipeline sequence
+// number) runs on slot stream g % depth (8 by default) with its own work queues,
+// overflow stack, tile order and camera-ray results, and writes its sample colours
+// to colour buffer g % (depth + 1). While other frames are in flight its persistent
+// grid is 1/depth of residency (renderOne), so the frames in flight share the GPU by
+// space: their waves are resident together, and a frame whose last long paths keep a
+// few waves busy leaves the rest of the machine to the others. Its running-mean
+// update (mixKernel) runs on the caller's stream, in frame order, once the frame's
+// kernel has ended: the accumulation is updated in frame order, the image is bit for
+// bit the one of serial frames, and whatever the caller queues behind a frame (pack,
+// download, tonemap) follows its update with no further cross-queue wait. No frame
+// kernel waits for a mix except the one of the frame depth + 1 back, whose colour
+// buffer it reuses. (Measured alternatives, DESIGN.md 4: a separate mix stream is
+// twice as slow at small shares -- each mix waited on two ~25 us cross-queue signals
+// in a chain from mix to mix; and with full-residency grids a mix waits for a CU slot
+// behind the next frame's persistent kernel, ~250 us on c2, which made deeper
+// pipelines slower, not faster.)
 #ifndef PT_PIPE
-#define PT_PIPE 2  // 1 (serial), 3 and 4 measured slower
+#define PT_PIPE 8  // frames in flight (PT_PIPE_DEPTH overrides; capped by the hardware queues)
 #endif
-static constexpr int PIPE = PT_PIPE;
+static constexpr int PIPE = MAX_SLOTS;      // most frames in flight
+static constexpr int COLS = MAX_SLOTS + 1;  // colour buffers (one more than the frames in flight)
+static_assert(PT_PIPE >= 1 && PT_PIPE <= PIPE, "PT_PIPE: 1..MAX_SLOTS");
 static_assert(PIPE * NUM_QUEUES * CTL_LINE_INTS * 4 <= (int)CTL_STATS, "queue counters of every slot fit the control block");
 
 #ifndef PT_TILE_GROUP
@@ -126,16 +138,21 @@ struct pt_ctx {
   unsigned sceneVersion = 0, binVersion = 0;
   // frames in flight (PIPE slots; see PIPE above)
   bool pipe = false;                        // this context pipelines its megakernel frames
+  int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
+  bool gridShare = true;                    // frames in flight split the persistent grid (PT_GRID_SHARE=0: not)
   hipStream_t slotStream[PIPE] = {};
-  hipEvent_t mixDone[PIPE] = {};            // slot's last running-mean update
-  hipEvent_t userMark = nullptr;            // the caller's stream at the last frame's call
+  hipEvent_t kernelDone[PIPE] = {};         // slot's last frame kernel (+ reorder) ended
+  bool slotBusy[PIPE] = {};                 // kernelDone[k] has been recorded since the last sync
+  hipEvent_t mixDone[COLS] = {};            // colour buffer's last running-mean update
+  hipStream_t lastMixStream = nullptr;      // the stream the last update ran on (pt_set_stream may change it)
   // camera-ray bins built on one slot's stream: binsBuilt is recorded after the build, and
   // every other slot waits for it once before its first frame with those bins (binGen)
   hipEvent_t binsBuilt = nullptr;
   unsigned binGen = 0, binGenSeen[MAX_SLOTS] = {};
-  float4* d_col[PIPE] = {};                 // per-slot sample colours
+  float4* d_col[COLS] = {};                 // per-colour-buffer sample colours
   int2* d_prim[PIPE] = {};                  // per-slot camera-ray results (primaryKernel)
   int lastSlot = -1;                        // slot of the last pipelined frame
+  int lastCol = -1;                         // colour buffer of the last pipelined frame
   bool mixPending = false;                  // a pipelined frame's update may still be running
   unsigned long long frameNo = 0;           // pipelined frames issued
   int probeN[4] = {0, 0, 0, 0};        // timed frames: runtime tree, uploaded tree (both unsplit), split, unordered
@@ -307,11 +324,17 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   ctx->pipe = cfg->integrator != PT_BASIC_CPU_COMPAT &&
               !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_WAVEFRONT | PT_FLAG_REGEN | PT_FLAG_SERIAL_FRAMES));
   if (ctx->pipe) {
-    CKC(hipEventCreateWithFlags(&ctx->userMark, hipEventDisableTiming));
-    for (int k = 0; k < PIPE; k++) {
-      CKC(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
-      CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
-    }
+    // a process has GPU_MAX_HW_QUEUES hardware queues (HIP's default 4; the Python package and
+    // bench.py ask for 12): streams beyond them share queues and serialise, so the slot streams,
+    // the context's own stream and the caller's (torch's) must fit
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
+    ctx->pipeDepth = std::min(ctx->pipeDepth, std::max(2, hwq - 2));
+    if (const char* e = std::getenv("PT_PIPE_DEPTH")) ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
+    // slot streams are created as a depth first uses them (ensureSlots): streams beyond the
+    // hardware queues share queues, which serialises their work
+    for (int k = 0; k < COLS; k++) CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
     CKC(hipEventCreateWithFlags(&ctx->binsBuilt, hipEventDisableTiming));
   }
 #undef CKC
@@ -381,12 +404,14 @@ void pt_destroy(pt_ctx* ctx) {
   freePrimaryBins(ctx->bins);
   for (int k = 0; k < PIPE; k++) {
     if (ctx->slotStream[k]) (void)hipStreamSynchronize(ctx->slotStream[k]);
-    dfree(ctx->d_col[k]);
     dfree(ctx->d_prim[k]);
-    if (ctx->mixDone[k]) (void)hipEventDestroy(ctx->mixDone[k]);
+    if (ctx->kernelDone[k]) (void)hipEventDestroy(ctx->kernelDone[k]);
     if (ctx->slotStream[k]) (void)hipStreamDestroy(ctx->slotStream[k]);
   }
-  if (ctx->userMark) (void)hipEventDestroy(ctx->userMark);
+  for (int k = 0; k < COLS; k++) {
+    dfree(ctx->d_col[k]);
+    if (ctx->mixDone[k]) (void)hipEventDestroy(ctx->mixDone[k]);
+  }
   if (ctx->binsBuilt) (void)hipEventDestroy(ctx->binsBuilt);
   freeWavefront(ctx);
   for (hipEvent_t e : ctx->ev)
@@ -1450,7 +1475,7 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
     // split state and cost estimates start over (the camera or scene changed), in
     // every slot's stream order (after its last reorder, before its next frame)
     if (ctx->d_cost)
-      for (int k = 0; k < (ctx->pipe ? PIPE : 1); k++)
+      for (int k = 0; k < (ctx->pipe ? ctx->pipeDepth : 1); k++)
         (void)hipMemsetAsync(ctx->d_cost + (size_t)k * 4 * ctx->numItems + 2 * (size_t)ctx->numItems, 0,
                              2 * (size_t)ctx->numItems * sizeof(int), ctx->pipe ? ctx->slotStream[k] : ctx->stream);
   }
@@ -1487,6 +1512,15 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
 }
 
 static PackParams packParams(const pt_ctx* ctx, int rank, int world);
+
+// the slot streams (and their events) of depth D
+static int ensureSlots(pt_ctx* ctx, int D) {
+  for (int k = 0; k < D; k++) {
+    if (!ctx->slotStream[k]) CK(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
+    if (!ctx->kernelDone[k]) CK(hipEventCreateWithFlags(&ctx->kernelDone[k], hipEventDisableTiming));
+  }
+  return PT_OK;
+}
 
 static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
   if (!ctx) return PT_E_INVALID;
@@ -1550,10 +1584,23 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + HIT_F4 * 16) + (size_t)ctx->nDevNodes * 64;
   const bool wideScene = !count && cull && c.integrator != 0 && sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
   const bool regen = !count && ((c.flags & PT_FLAG_REGEN) || (wideScene && !(c.flags & PT_FLAG_MEGAKERNEL)));
-  // this frame's stream and per-frame buffers: slot frameNo % PIPE when pipelined
+  // this frame's stream and per-frame buffers: slot frameNo % depth, colour buffer
+  // frameNo % (depth + 1) when pipelined
   const bool piped = ctx->pipe && !count;
-  const int slot = piped ? (int)(ctx->frameNo % PIPE) : 0;
+  if (piped) {
+    if (int e = ensureSlots(ctx, ctx->pipeDepth)) return e;
+  }
+  const int D = piped ? ctx->pipeDepth : 1;
+  const int slot = piped ? (int)(ctx->frameNo % (unsigned)D) : 0;
+  const int colIdx = piped ? (int)(ctx->frameNo % (unsigned)(D + 1)) : 0;
   hipStream_t S = piped ? ctx->slotStream[slot] : ctx->stream;
+  // every other slot's frame in flight has ended on S (the frames that read buffers
+  // rebuilt below)
+  auto waitOthers = [&]() -> int {
+    for (int k = 0; k < D; k++)
+      if (k != slot && ctx->slotBusy[k]) CK(hipStreamWaitEvent(S, ctx->kernelDone[k], 0));
+    return PT_OK;
+  };
   int nb = 0;
   const bool wide = wideScene;  // the more-waves variant of either kernel
   if (regen) CK(regenBlocksPerCU(c.integrator, cull, wide, &nb));
@@ -1561,12 +1608,27 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (nb < 1) nb = 1;
   ctx->lastWaves = nb * BLOCK / 64 / 4;  // 4 SIMDs per CU
   ctx->lastRegen = regen;
-  int grid = ctx->numCU * nb;
+  // Frames in flight share the GPU by space, not by time: a frame's persistent grid is
+  // residency / (frames in flight), so the frames' waves are all resident together and a
+  // frame whose long paths keep a few waves busy leaves the rest of the machine to the
+  // others (and to the running-mean updates). A persistent grid sized to all of residency
+  // keeps the next frame's waves -- and every other launch -- waiting for its tail: c4
+  // 0.48 -> 0.34 ms per frame at 8 frames in flight, c2's 1/8 screen share 0.096 -> 0.072.
+  // A caller that waits for every frame gets the whole machine for each.
+  const int fullGrid = ctx->numCU * nb;
+  int grid = fullGrid;
+  if (piped && D > 1 && ctx->gridShare) {
+    bool others = false;  // another frame still in flight: the caller streams frames
+    for (int k = 0; k < D && !others; k++)
+      others = k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
+    (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
+    if (others) grid = std::max(NUM_QUEUES, fullGrid / D);
+  }
   int ovfDepth = 0;
-  int rc = ensureOverflow(ctx, (size_t)grid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, piped ? PIPE : 1);
+  int rc = ensureOverflow(ctx, (size_t)fullGrid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
   if (rc) return rc;
   const size_t npix = (size_t)c.width * c.height;
-  if (piped && !ctx->d_col[slot]) CK(hipMalloc(&ctx->d_col[slot], npix * sizeof(float4)));
+  if (piped && !ctx->d_col[colIdx]) CK(hipMalloc(&ctx->d_col[colIdx], npix * sizeof(float4)));
   int* queue = reinterpret_cast<int*>(ctx->d_ctl + CTL_QUEUES) + (size_t)slot * NUM_QUEUES * CTL_LINE_INTS;
   CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   RenderParams p;
@@ -1585,7 +1647,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   std::memcpy(p.eye, eye, sizeof(p.eye));
   std::memcpy(p.cam, cameraRotate, sizeof(p.cam));
   p.accum = ctx->d_accum;
-  p.col = piped ? ctx->d_col[slot] : nullptr;
+  p.col = piped ? ctx->d_col[colIdx] : nullptr;
   p.queue = queue;
   p.perQueue = ctx->perQueue;
   p.numItems = ctx->numItems;
@@ -1594,7 +1656,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.shardsX = ctx->shardsX;
   p.rank = c.tile_rank;
   p.world = c.tile_world;
-  p.ovf = ovfDepth ? ctx->d_ovf + (size_t)slot * grid * BLOCK * ovfDepth : nullptr;
+  p.ovf = ovfDepth ? ctx->d_ovf + (size_t)slot * fullGrid * BLOCK * ovfDepth : nullptr;
   p.ovfDepth = ovfDepth;
   p.scene.fast = 0;  // probePolicy below
 
@@ -1642,7 +1704,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (bins) {
     if (!ctx->binsValid || ctx->binVersion != ctx->sceneVersion || std::memcmp(ctx->binEye, eye, sizeof(ctx->binEye)) ||
         std::memcmp(ctx->binCam, cameraRotate, sizeof(ctx->binCam))) {
-      if (ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
+      if (piped) {
+        if (int e = waitOthers()) return e;
+      }
       ctx->binsValid = false;
       CK(buildPrimaryBins(eye, cameraRotate, c.width, c.height, ctx->d_geo, ctx->nTri, ctx->bins, S));
       std::memcpy(ctx->binEye, eye, sizeof(ctx->binEye));
@@ -1684,7 +1748,11 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // a pipelined frame still starts only after the previous one has ended.
   const bool probing = ordered && PT_SPLIT_AUTO &&
                        (ctx->treeDecided < 0 || ctx->splitDecided < 0 || ctx->orderDecided < 0);
-  if (piped && probing && ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
+  if (piped && probing) {
+    if (int e = waitOthers()) return e;
+  }
+  // the colour buffer's previous frame (depth + 1 back) has been mixed
+  if (piped && ctx->frameNo >= (unsigned long long)(D + 1)) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
   int erc = launchEvents(ctx, &evb, &eve);
   if (erc) return erc;
 #if PT_WAVE_TRACE
@@ -1726,17 +1794,18 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // policy probe weighs the order's cost too; the running-mean update below is not in it
   CK(hipEventRecord(eve, S));
   if (piped) {
-    // the running-mean update, in frame order: after the previous frame's update and
-    // after whatever the caller's stream held when this frame was requested
-    CK(hipEventRecord(ctx->userMark, ctx->stream));
-    CK(hipStreamWaitEvent(S, ctx->userMark, 0));
-    if (ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastSlot], 0));
-    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[slot], frameCounter, S));
-    CK(hipEventRecord(ctx->mixDone[slot], S));
-    // the caller's stream is ordered after this frame (pt_abi.h: stream-ordered calls);
-    // the slot streams' next frame kernels do not wait on it
-    CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[slot], 0));
+    // the running-mean update on the caller's stream, in frame order, after this frame's kernel
+    CK(hipEventRecord(ctx->kernelDone[slot], S));
+    ctx->slotBusy[slot] = true;
+    CK(hipStreamWaitEvent(ctx->stream, ctx->kernelDone[slot], 0));
+    if (ctx->mixPending && ctx->lastMixStream != ctx->stream)  // the caller switched streams: keep frame order
+      CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastCol], 0));
+    ctx->lastMixStream = ctx->stream;
+    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[colIdx], frameCounter,
+                 ctx->stream));
+    CK(hipEventRecord(ctx->mixDone[colIdx], ctx->stream));
     ctx->lastSlot = slot;
+    ctx->lastCol = colIdx;
     ctx->mixPending = true;
     ctx->frameNo++;
   }
@@ -1748,15 +1817,17 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
 static int joinPipe(pt_ctx* ctx) {
   if (!ctx->mixPending) return PT_OK;
   CK(hipSetDevice(ctx->cfg.device_id));
-  CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastSlot], 0));
+  CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastCol], 0));
   return PT_OK;
 }
 
 // every stream the context renders on, then its own: all work done
 static int syncStreams(pt_ctx* ctx) {
   CK(hipSetDevice(ctx->cfg.device_id));
-  for (int k = 0; k < PIPE; k++)
+  for (int k = 0; k < PIPE; k++) {
     if (ctx->slotStream[k]) CK(hipStreamSynchronize(ctx->slotStream[k]));
+    ctx->slotBusy[k] = false;
+  }
   CK(hipStreamSynchronize(ctx->stream));
   ctx->mixPending = false;
   return PT_OK;
@@ -2020,13 +2091,13 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->regen = ctx->lastRegen ? 1 : 0;
   st->devices = 1;
   st->gather = 0;
-  st->frames_in_flight = ctx->pipe ? PIPE : 1;
+  st->frames_in_flight = ctx->pipe ? ctx->pipeDepth : 1;
   st->upload_ms = ctx->uploadMs;
   st->accel_build_ms = ctx->accelMs;
   st->accel_device = ctx->accelDevice;
   st->accel_nodes = ctx->accelNodes;
   st->accel_depth = ctx->accelDepth;
-  const int ls = ctx->pipe && ctx->frameNo > 0 ? (int)((ctx->frameNo - 1) % PIPE) : 0;  // the last frame's slot
+  const int ls = ctx->pipe && ctx->frameNo > 0 ? ctx->lastSlot : 0;  // the last frame's slot
   if (ctx->d_order && ctx->orderValid[ls]) {
     int counts[NUM_QUEUES];
     const int* ord = ctx->d_order + (size_t)ls * ((size_t)NUM_QUEUES * ctx->orderCap + NUM_QUEUES);

@@ -2,6 +2,10 @@ import os
 import sys
 from pathlib import Path
 
+# hardware queues for the renderer's frames in flight, before anything initialises HIP
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import opengl_ray_tracing_amd  # noqa: E402,F401
+
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent

@@ -251,13 +251,17 @@ def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
     assert sl.regen == 0
 
 
-@pytest.mark.parametrize("name,tile", [("c4", (0, 1)), ("c2", (1, 3))])
-def test_pipelined_frames_equal_serial_frames(request, name, tile):
+@pytest.mark.parametrize("name,tile,depth", [("c4", (0, 1), None), ("c2", (1, 3), None), ("c4", (0, 1), 3),
+                                              ("c2", (1, 3), 8)])
+def test_pipelined_frames_equal_serial_frames(request, monkeypatch, name, tile, depth):
     """Frames in flight (the default: frame f+1's megakernel overlaps frame f's tail, each
     frame's running-mean update runs in frame order) give the image of serial frames
-    (PT_FLAG_SERIAL_FRAMES) bit for bit -- through the policy probe, a camera reset, images
-    read mid-stream and a screen-tile shard -- with the same rays."""
+    (PT_FLAG_SERIAL_FRAMES) bit for bit -- through the policy probes (the depth probe drains
+    and changes the pipeline depth mid-stream), a camera reset, images read mid-stream and a
+    screen-tile shard, and at fixed depths 3 and 8 (PT_PIPE_DEPTH) -- with the same rays."""
     from opengl_ray_tracing_amd import FLAG_SERIAL_FRAMES
+    if depth is not None:
+        monkeypatch.setenv("PT_PIPE_DEPTH", str(depth))
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     eye, rot = orbit_camera(*cfg.camera)
     eye2, rot2 = orbit_camera(30.0, 15.0, 4.0)
@@ -279,7 +283,8 @@ def test_pipelined_frames_equal_serial_frames(request, name, tile):
 
     a, sa = run(0)
     b, sb = run(FLAG_SERIAL_FRAMES)
-    assert sa.frames_in_flight == 2 and sb.frames_in_flight == 1
+    assert sa.frames_in_flight == (depth or sa.frames_in_flight) and sa.frames_in_flight >= 2
+    assert sb.frames_in_flight == 1
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert sa.rays == sb.rays

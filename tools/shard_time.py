@@ -13,6 +13,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
+import os  # noqa: E402
+
+import opengl_ray_tracing_amd  # noqa: E402,F401  (raises GPU_MAX_HW_QUEUES before HIP initialises)
 
 
 def main():
@@ -32,13 +35,13 @@ def main():
                       tile_world=n) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
-            for f in range(24):  # policy probe + warmup
+            for f in range(100):  # policy probe (tree, split, order, depth) + warmup
                 r.render_frame(eye, rot, f, sync=False)
             r.synchronize()
             r.reset_stats()
             K = 100
             t0 = time.perf_counter()
-            for f in range(24, 24 + K):
+            for f in range(100, 100 + K):
                 r.render_frame(eye, rot, f, sync=False)
             t_sub = time.perf_counter()
             r.synchronize()
@@ -48,7 +51,8 @@ def main():
         print(json.dumps({"variant": os.environ.get("PT_VARIANT", "base"), "config": cfg_name, "world": n, "rank0_ms_per_frame": round(ms, 4),
                           "kernel_ms_avg": round(st.kernel_ms_total / max(st.launches, 1), 4),
                           "host_submit_ms": round(submit_ms, 4),
-                          "rays_per_frame": st.rays // max(st.launches, 1)}), flush=True)
+                          "rays_per_frame": st.rays // max(st.launches, 1),
+                          "frames_in_flight": st.frames_in_flight}), flush=True)
 
 
 if __name__ == "__main__":
