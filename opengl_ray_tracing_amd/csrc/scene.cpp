@@ -5,6 +5,7 @@
 // match what the reference host program would upload (OpenglRayTracing/main.cpp).
 #include "pt_scene.h"
 #include "pt_accel.h"
+#include "pt_introsort.h"
 
 #include <algorithm>
 #include <cmath>
@@ -198,88 +199,206 @@ int new_node(std::vector<BVHNode>& nodes) {
   return id;
 }
 
-// buildBVH (main.cpp:376-427): split at the median of the longest axis.
-int splitMedian(std::vector<Triangle>& tr, const BVHNode& node, int l, int r, bool) {
-  float lenx = node.BB.x - node.AA.x;
-  float leny = node.BB.y - node.AA.y;
-  float lenz = node.BB.z - node.AA.z;
-  if (lenx >= leny && lenx >= lenz) std::sort(tr.begin() + l, tr.begin() + r + 1, CmpAxis{0});
-  if (leny >= lenx && leny >= lenz) std::sort(tr.begin() + l, tr.begin() + r + 1, CmpAxis{1});
-  if (lenz >= lenx && lenz >= leny) std::sort(tr.begin() + l, tr.begin() + r + 1, CmpAxis{2});
-  return (l + r) / 2;
+// appends a privately built subtree (ids from 1) to nodes, preserving preorder
+int splice(std::vector<BVHNode>& nodes, const std::vector<BVHNode>& local, int root) {
+  if (root == 0) return 0;
+  const int shift = (int)nodes.size() - 1;  // local ids start at 1 (slot 0 is a placeholder)
+  for (size_t k = 1; k < local.size(); k++) {
+    BVHNode x = local[k];
+    if (x.left > 0) x.left += shift;
+    if (x.right > 0) x.right += shift;
+    nodes.push_back(x);
+  }
+  return root + shift;
 }
 
-// buildBVHwithSAH (main.cpp:430-551). zTypo reproduces main.cpp:480,484
-// (t.p2.x in the z prefix bounds).
-int splitSAH(std::vector<Triangle>& tr, const BVHNode&, int l, int r, bool zTypo) {
-  float Cost = kINF;
-  int Axis = 0;
-  int Split = (l + r) / 2;
-  const int cnt = r - l + 1;
-  std::vector<f3> leftMax(cnt), leftMin(cnt), rightMax(cnt), rightMin(cnt);
-  for (int axis = 0; axis < 3; axis++) {
-    std::sort(&tr[0] + l, &tr[0] + r + 1, CmpAxis{axis});
-    for (int k = 0; k < cnt; k++) {
-      leftMax[k] = F3(-kINF, -kINF, -kINF); leftMin[k] = F3(kINF, kINF, kINF);
-      rightMax[k] = F3(-kINF, -kINF, -kINF); rightMin[k] = F3(kINF, kINF, kINF);
+// ---- the reference builders (buildBVH main.cpp:376-427, buildBVHwithSAH main.cpp:430-551)
+// The reference sorts Triangle records with std::sort by centre. Here the recursion orders
+// triangle ids instead: (centre, id) pairs compared by centre make the same comparisons, so
+// pt::exactSort (std::sort's permutation, computed in parallel -- pt_introsort.h) leaves the
+// ids in the order the records would be in, and the per-triangle bounds the SAH sweeps read
+// come from flat arrays rather than 140-byte records.
+struct TriBox {
+  float lo[3], hi[3];  // min / max over the three vertices
+  float loZL, hiZL;    // the SAH left sweep's z bounds: main.cpp:480,484 read p2.x
+};
+struct RefInput {
+  std::vector<float> c[3];  // centre per axis (main.cpp:152-166)
+  std::vector<TriBox> box;  // one 32-byte record per triangle: a sweep step reads one line
+};
+RefInput ref_input(const std::vector<Triangle>& tr) {
+  RefInput in;
+  const size_t n = tr.size();
+  for (int a = 0; a < 3; a++) in.c[a].resize(n);
+  in.box.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    const Triangle& t = tr[i];
+    for (int a = 0; a < 3; a++) in.c[a][i] = centre(t, a);
+    TriBox& b = in.box[i];
+    b.lo[0] = gmin(t.p1.x, gmin(t.p2.x, t.p3.x));
+    b.lo[1] = gmin(t.p1.y, gmin(t.p2.y, t.p3.y));
+    b.lo[2] = gmin(t.p1.z, gmin(t.p2.z, t.p3.z));
+    b.hi[0] = gmax(t.p1.x, gmax(t.p2.x, t.p3.x));
+    b.hi[1] = gmax(t.p1.y, gmax(t.p2.y, t.p3.y));
+    b.hi[2] = gmax(t.p1.z, gmax(t.p2.z, t.p3.z));
+    b.loZL = gmin(t.p1.z, gmin(t.p2.x, t.p3.z));
+    b.hiZL = gmax(t.p1.z, gmax(t.p2.x, t.p3.z));
+  }
+  return in;
+}
+struct KeyId {
+  float k;
+  int id;
+};
+struct KeyLess {
+  bool operator()(const KeyId& a, const KeyId& b) const { return a.k < b.k; }
+};
+enum class RefKind { Median, SAH, FixedSAH };
+
+struct RefScratch {
+  std::vector<KeyId> kv;
+  std::vector<float> right;  // suffix bounds of the SAH sweep, 6 per position
+};
+
+class RefBuilder {
+ public:
+  RefBuilder(const RefInput& in, RefKind kind, int leaf, int* id, pt::Helpers* h)
+      : in_(in), kind_(kind), leaf_(leaf), id_(id), h_(h) {}
+
+  // the recursion of main.cpp:376-427 / 430-551 with preorder node ids
+  int build(std::vector<BVHNode>& nodes, int l, int r, RefScratch& s) {
+    if (l > r) return 0;
+    const int nid = new_node(nodes);
+    bounds(l, r, nodes[nid]);
+    if ((r - l + 1) <= leaf_) {
+      nodes[nid].n = r - l + 1;
+      nodes[nid].index = l;
+      return nid;
     }
+    const int mid = kind_ == RefKind::Median ? splitMedian(nodes[nid], l, r, s) : splitSAH(l, r, s);
+    int left, right;
+    if (std::min(mid - l + 1, r - mid) >= kParMin && h_->take()) {
+      std::vector<BVHNode> ln(1), rn(1);
+      int lr = 0;
+      std::thread th([&] {
+        RefScratch s2;
+        lr = build(ln, l, mid, s2);
+        h_->give();
+      });
+      const int rr = build(rn, mid + 1, r, s);
+      th.join();
+      left = splice(nodes, ln, lr);
+      right = splice(nodes, rn, rr);
+    } else {
+      left = build(nodes, l, mid, s);
+      right = build(nodes, mid + 1, r, s);
+    }
+    nodes[nid].left = left;
+    nodes[nid].right = right;
+    return nid;
+  }
+
+ private:
+  static constexpr int kParMin = 4096;
+
+  void bounds(int l, int r, BVHNode& node) const {
+    node.AA = F3(kINF, kINF, kINF);
+    node.BB = F3(-kINF, -kINF, -kINF);
     for (int i = l; i <= r; i++) {
-      const Triangle& t = tr[i];
-      int bias = (i == l) ? 0 : 1;
-      const f3& pM = leftMax[i - l - bias];
-      const f3& pm = leftMin[i - l - bias];
-      float zx = zTypo ? t.p2.x : t.p2.z;
-      f3 M, m;
-      M.x = gmax(pM.x, gmax(t.p1.x, gmax(t.p2.x, t.p3.x)));
-      M.y = gmax(pM.y, gmax(t.p1.y, gmax(t.p2.y, t.p3.y)));
-      M.z = gmax(pM.z, gmax(t.p1.z, gmax(zx, t.p3.z)));
-      m.x = gmin(pm.x, gmin(t.p1.x, gmin(t.p2.x, t.p3.x)));
-      m.y = gmin(pm.y, gmin(t.p1.y, gmin(t.p2.y, t.p3.y)));
-      m.z = gmin(pm.z, gmin(t.p1.z, gmin(zx, t.p3.z)));
-      leftMax[i - l] = M;
-      leftMin[i - l] = m;
-    }
-    for (int i = r; i >= l; i--) {
-      const Triangle& t = tr[i];
-      int bias = (i == r) ? 0 : 1;
-      const f3& pM = rightMax[i - l + bias];
-      const f3& pm = rightMin[i - l + bias];
-      f3 M, m;
-      M.x = gmax(pM.x, gmax(t.p1.x, gmax(t.p2.x, t.p3.x)));
-      M.y = gmax(pM.y, gmax(t.p1.y, gmax(t.p2.y, t.p3.y)));
-      M.z = gmax(pM.z, gmax(t.p1.z, gmax(t.p2.z, t.p3.z)));
-      m.x = gmin(pm.x, gmin(t.p1.x, gmin(t.p2.x, t.p3.x)));
-      m.y = gmin(pm.y, gmin(t.p1.y, gmin(t.p2.y, t.p3.y)));
-      m.z = gmin(pm.z, gmin(t.p1.z, gmin(t.p2.z, t.p3.z)));
-      rightMax[i - l] = M;
-      rightMin[i - l] = m;
-    }
-    float cost = kINF;
-    int split = l;
-    for (int i = l; i <= r - 1; i++) {
-      f3 lA = leftMin[i - l], lB = leftMax[i - l];
-      float lenx = lB.x - lA.x, leny = lB.y - lA.y, lenz = lB.z - lA.z;
-      float leftS = (float)(2.0 * (double)((lenx * leny) + (lenx * lenz) + (leny * lenz)));
-      float leftCost = leftS * (float)(i - l + 1);
-      f3 rA = rightMin[i + 1 - l], rB = rightMax[i + 1 - l];
-      lenx = rB.x - rA.x; leny = rB.y - rA.y; lenz = rB.z - rA.z;
-      float rightS = (float)(2.0 * (double)((lenx * leny) + (lenx * lenz) + (leny * lenz)));
-      float rightCost = rightS * (float)(r - i);
-      float totalCost = leftCost + rightCost;
-      if (totalCost < cost) {
-        cost = totalCost;
-        split = i;
-      }
-    }
-    if (cost < Cost) {
-      Cost = cost;
-      Axis = axis;
-      Split = split;
+      const TriBox& b = in_.box[id_[i]];
+      node.AA.x = gmin(node.AA.x, b.lo[0]);
+      node.AA.y = gmin(node.AA.y, b.lo[1]);
+      node.AA.z = gmin(node.AA.z, b.lo[2]);
+      node.BB.x = gmax(node.BB.x, b.hi[0]);
+      node.BB.y = gmax(node.BB.y, b.hi[1]);
+      node.BB.z = gmax(node.BB.z, b.hi[2]);
     }
   }
-  std::sort(&tr[0] + l, &tr[0] + r + 1, CmpAxis{Axis});
-  return Split;  // the prefix arrays are freed before recursing (the reference keeps them: memory only)
-}
+
+  // std::sort(tr + l, tr + r + 1, cmpx|cmpy|cmpz), on the ids. A range already strictly
+  // increasing in the key is its own (unique) sorted order: no sort needed.
+  void sortAxis(int l, int r, int axis, RefScratch& s) {
+    const int cnt = r - l + 1;
+    const float* key = in_.c[axis].data();
+    s.kv.resize((size_t)cnt);
+    bool strict = true;
+    for (int i = 0; i < cnt; i++) {
+      const int t = id_[l + i];
+      s.kv[i] = KeyId{key[t], t};
+      if (i && !(s.kv[i - 1].k < s.kv[i].k)) strict = false;
+    }
+    if (strict) return;
+    pt::exactSort(s.kv.data(), s.kv.data() + cnt, KeyLess{}, cnt >= (1 << 16) ? h_ : nullptr);
+    for (int i = 0; i < cnt; i++) id_[l + i] = s.kv[i].id;
+  }
+
+  int splitMedian(const BVHNode& node, int l, int r, RefScratch& s) {
+    float lenx = node.BB.x - node.AA.x;
+    float leny = node.BB.y - node.AA.y;
+    float lenz = node.BB.z - node.AA.z;
+    if (lenx >= leny && lenx >= lenz) sortAxis(l, r, 0, s);
+    if (leny >= lenx && leny >= lenz) sortAxis(l, r, 1, s);
+    if (lenz >= lenx && lenz >= leny) sortAxis(l, r, 2, s);
+    return (l + r) / 2;
+  }
+
+  int splitSAH(int l, int r, RefScratch& s) {
+    const bool zTypo = kind_ == RefKind::SAH;
+    float Cost = kINF;
+    int Axis = 0;
+    int Split = (l + r) / 2;
+    const int cnt = r - l + 1;
+    s.right.resize((size_t)cnt * 6);
+    float* R = s.right.data();
+    for (int axis = 0; axis < 3; axis++) {
+      sortAxis(l, r, axis, s);
+      // suffix bounds (main.cpp:487-503)
+      float Mx = -kINF, My = -kINF, Mz = -kINF, mx = kINF, my = kINF, mz = kINF;
+      for (int i = r; i >= l; i--) {
+        const TriBox& b = in_.box[id_[i]];
+        Mx = gmax(Mx, b.hi[0]); My = gmax(My, b.hi[1]); Mz = gmax(Mz, b.hi[2]);
+        mx = gmin(mx, b.lo[0]); my = gmin(my, b.lo[1]); mz = gmin(mz, b.lo[2]);
+        float* o = R + (size_t)(i - l) * 6;
+        o[0] = Mx; o[1] = My; o[2] = Mz; o[3] = mx; o[4] = my; o[5] = mz;
+      }
+      // prefix bounds (main.cpp:471-485) and the cost sweep (main.cpp:505-534)
+      Mx = My = Mz = -kINF;
+      mx = my = mz = kINF;
+      float cost = kINF;
+      int split = l;
+      for (int i = l; i <= r - 1; i++) {
+        const TriBox& b = in_.box[id_[i]];
+        Mx = gmax(Mx, b.hi[0]); My = gmax(My, b.hi[1]); Mz = gmax(Mz, zTypo ? b.hiZL : b.hi[2]);
+        mx = gmin(mx, b.lo[0]); my = gmin(my, b.lo[1]); mz = gmin(mz, zTypo ? b.loZL : b.lo[2]);
+        float lenx = Mx - mx, leny = My - my, lenz = Mz - mz;
+        float leftS = (float)(2.0 * (double)((lenx * leny) + (lenx * lenz) + (leny * lenz)));
+        float leftCost = leftS * (float)(i - l + 1);
+        const float* o = R + (size_t)(i + 1 - l) * 6;
+        lenx = o[0] - o[3]; leny = o[1] - o[4]; lenz = o[2] - o[5];
+        float rightS = (float)(2.0 * (double)((lenx * leny) + (lenx * lenz) + (leny * lenz)));
+        float rightCost = rightS * (float)(r - i);
+        float totalCost = leftCost + rightCost;
+        if (totalCost < cost) {
+          cost = totalCost;
+          split = i;
+        }
+      }
+      if (cost < Cost) {
+        Cost = cost;
+        Axis = axis;
+        Split = split;
+      }
+    }
+    sortAxis(l, r, Axis, s);  // main.cpp:537-544
+    return Split;
+  }
+
+  const RefInput& in_;
+  RefKind kind_;
+  int leaf_;
+  int* id_;
+  pt::Helpers* h_;
+};
 
 // Binned SAH (32 bins over centroid bounds), O(n log n). Not a reference
 // routine: a fast builder for the 1M-triangle stress scene. Same node
@@ -361,18 +480,6 @@ int splitBinned(std::vector<Triangle>& tr, const BVHNode&, int l, int r, bool) {
 // node array and the triangle order are identical to a serial build.
 typedef int (*SplitFn)(std::vector<Triangle>&, const BVHNode&, int, int, bool);
 constexpr int kParMin = 8192;
-
-int splice(std::vector<BVHNode>& nodes, const std::vector<BVHNode>& local, int root) {
-  if (root == 0) return 0;
-  const int shift = (int)nodes.size() - 1;  // local ids start at 1 (slot 0 is a placeholder)
-  for (size_t k = 1; k < local.size(); k++) {
-    BVHNode x = local[k];
-    if (x.left > 0) x.left += shift;
-    if (x.right > 0) x.right += shift;
-    nodes.push_back(x);
-  }
-  return root + shift;
-}
 
 int buildTree(std::vector<Triangle>& tr, std::vector<BVHNode>& nodes, int l, int r, int n, SplitFn split, bool flag,
               int parDepth) {
@@ -618,17 +725,29 @@ int pt_scene_build_bvh(pt_scene* s, int builder, int leafSize) {
   testNode.BB = F3(0, 1, 0);
   s->nodes.assign(1, testNode);
   s->nodes.reserve(2 * s->triangles.size() / (size_t)leafSize + 16);
-  int r = (int)s->triangles.size() - 1;
-  // threads: up to 2^parDepth subtrees in flight
+  const int r = (int)s->triangles.size() - 1;
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  int parDepth = 0;
-  while ((1u << parDepth) < hw) parDepth++;
-  switch (builder) {
-    case PT_BVH_REFERENCE_SAH: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitSAH, true, parDepth); break;
-    case PT_BVH_REFERENCE_MEDIAN: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitMedian, false, parDepth); break;
-    case PT_BVH_FIXED_SAH: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitSAH, false, parDepth); break;
-    case PT_BVH_BINNED_SAH: buildTree(s->triangles, s->nodes, 0, r, leafSize, splitBinned, false, parDepth); break;
-    default: return -1;
+  if (builder == PT_BVH_BINNED_SAH) {
+    int parDepth = 0;  // up to 2^parDepth subtrees in flight
+    while ((1u << parDepth) < hw) parDepth++;
+    buildTree(s->triangles, s->nodes, 0, r, leafSize, splitBinned, false, parDepth);
+  } else {
+    RefKind kind;
+    switch (builder) {
+      case PT_BVH_REFERENCE_SAH: kind = RefKind::SAH; break;
+      case PT_BVH_REFERENCE_MEDIAN: kind = RefKind::Median; break;
+      case PT_BVH_FIXED_SAH: kind = RefKind::FixedSAH; break;
+      default: return -1;
+    }
+    const RefInput in = ref_input(s->triangles);
+    std::vector<int> id((size_t)r + 1);
+    for (int i = 0; i <= r; i++) id[i] = i;
+    pt::Helpers helpers((int)hw - 1);
+    RefScratch scratch;
+    RefBuilder(in, kind, leafSize, id.data(), &helpers).build(s->nodes, 0, r, scratch);
+    std::vector<Triangle> built((size_t)r + 1);
+    for (int i = 0; i <= r; i++) built[i] = s->triangles[id[i]];
+    s->triangles.swap(built);
   }
   s->depth = tree_depth(s->nodes);
   return 0;
