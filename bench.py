@@ -23,7 +23,7 @@ N > 1 ranks (one process per GPU):
 Rank 0 prints one JSON line (contract in the task statement), with
 ``roofline`` for the frame kernel: the per-launch work the hardware counters
 measured for it (VALU wave-instructions, DRAM-side bytes; committed under
-profiles/r2/counters.json by tools/roofline.py) over its live HIP-event
+profiles/r3/counters.json by tools/roofline.py) over its live HIP-event
 duration, against each resource's peak -- ``bound`` is the resource with the
 highest fraction -- plus ``equivalent_GBs``, the reference algorithm's fetch
 bytes per launch over the same duration; and ``cpu_baseline``
@@ -53,6 +53,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_GINST = 1024 * 2.4 / 2 * 1e9 / 1e9
 METRIC = "Mrays/sec + ms/frame (1 spp, 1080p) at 1/2/4/8 MI355X; CPU-ref spp-matched PSNR"
 PROBE_FRAMES = 90  # frames after a restart during which the renderer measures its policies (tree, split, order, depth)
+SERIAL_FRAMES = 20  # frames of the serial-frames run behind roofline.kernel_basis
 
 
 def parse():
@@ -66,9 +67,12 @@ def parse():
     ap.add_argument("--no-psnr", action="store_true", help="skip the spp-matched PSNR check")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="cpu_baseline sample: full frames are rendered until this much CPU wall time has passed")
-    ap.add_argument("--counters", default=str(ROOT / "profiles" / "r2" / "counters.json"),
+    ap.add_argument("--counters", default=str(ROOT / "profiles" / "r3" / "counters.json"),
                     help="per-launch PMC counters of the bench kernel per config (tools/roofline.py)")
     ap.add_argument("--no-reset", action="store_true", help="skip the reset_ms_per_frame frames (profiling runs)")
+    ap.add_argument("--no-serial", action="store_true", help="skip the serial-frames run (roofline.kernel_basis)")
+    ap.add_argument("--cpu-all-seconds", type=float, default=4.0,
+                    help="cpu_baseline.all_cores sample: full frames at nproc threads for this long (0: skip)")
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="rehearsal: every rank on device 0")
@@ -175,6 +179,26 @@ def main():
             step(f, moved)
         sync_all()
         reset_ms = 1e3 * (time.perf_counter() - t2) / PROBE_FRAMES
+    # the frame kernel's own duration with nothing overlapping it: the same workload with frames
+    # issued serially (PT_FLAG_SERIAL_FRAMES, full-residency grid), HIP events around each launch.
+    # With frames in flight a launch's duration spans the frames it overlaps, so the roofline's
+    # second basis (kernel_basis) divides the same per-launch work by this serial duration.
+    serial_ms = None
+    if rank == 0 and n == 1 and not args.no_serial:
+        from opengl_ray_tracing_amd import FLAG_SERIAL_FRAMES
+        with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=local,
+                      flags=args.flags | FLAG_SERIAL_FRAMES) as rs:
+            rs.upload_scene(tris, nodes)
+            rs.upload_env(hdr)
+            for f in range(PROBE_FRAMES):
+                rs.render_frame(eye, rot, f, sync=False)
+            rs.synchronize()
+            rs.reset_stats()
+            for f in range(SERIAL_FRAMES):
+                rs.render_frame(eye, rot, PROBE_FRAMES + f, sync=False)
+            rs.synchronize()
+            ss = rs.stats()
+            serial_ms = ss.kernel_ms_total / max(ss.launches, 1)
     combined_finite = None
     if combine is not None:  # the ranks' running means -> one image on rank 0 (after the timed steps)
         img = combine()
@@ -215,9 +239,15 @@ def main():
                                   else "frame kernel HIP-event ms")
         roofline["launch_ms"] = round(kernel_ms_avg, 4)
         roofline["kernel"] = ("regenKernel<%s>" if st.regen else "renderKernel<%s>") % cfg.integrator
+        if serial_ms is not None:
+            kb = make_roofline(args, cfg, serial_ms, rays_per_launch, bytes_per_ray, n)
+            roofline["kernel_basis"] = {
+                "time_basis": "frame kernel HIP-event ms, frames issued serially (PT_FLAG_SERIAL_FRAMES)",
+                "kernel_ms": round(serial_ms, 4), "frames": SERIAL_FRAMES, "bound": kb["bound"],
+                "frac": kb["frac"], "candidates": kb.get("candidates"), "equivalent_GBs": kb["equivalent_GBs"]}
         cpu = None
         if not args.no_cpu_baseline and n == 1:
-            cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_seconds)
+            cpu = cpu_baseline(cfg, tris, nodes, hdr, eye, rot, args.cpu_seconds, args.cpu_all_seconds)
         quality = spp_matched_psnr(local) if not args.no_psnr else None
         line = {
             "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
@@ -251,7 +281,7 @@ def main():
 
 def make_roofline(args, cfg, kernel_ms, rays_per_launch, bytes_per_ray, n):
     """Roofline of the frame kernel. Each resource's per-launch work comes from the hardware
-    counters of the same workload (profiles/r2/counters.json, tools/roofline.py, one rocprofv3
+    counters of the same workload (profiles/r3/counters.json, tools/roofline.py, one rocprofv3
     pass per counter group over this bench's timed frames); divided by this run's live kernel
     time it gives the achieved rate:
       valu: SQ_INSTS_VALU wave-instructions / t  vs 1228.8 G/s (1024 SIMDs x 2.4 GHz / 2 cycles)
@@ -322,7 +352,7 @@ def spp_matched_psnr(device: int, spp: int = 128):
             "render_ms": round(dt * 1e3, 2)}
 
 
-def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, seconds):
+def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, seconds, all_seconds=0.0):
     """The CPU restatement of the reference (oracle/, test infrastructure) timed on the host
     cores: full frames of the same workload (same scene, camera, frame sequence), OpenMP over
     pixels, until `seconds` of wall time have passed (a bounded sample)."""
@@ -332,21 +362,29 @@ def cpu_baseline(cfg, tris, nodes, hdr, eye, rot, seconds):
     host = host_cpu()
     cores = host["threads"]
     orc = oracle.Oracle(tris, nodes, hdr)
-    acc = np.zeros((cfg.height, cfg.width, 4), np.float32)
-    rays = 0
-    frames = 0
-    t0 = time.perf_counter()
-    while True:
-        acc, c = orc.render(cfg.width, cfg.height, cfg.integrator, frames, eye, rot, accum=acc,
-                            max_bounce=cfg.max_bounce, threads=cores)
-        rays += c.rays
-        frames += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"{frames} full {cfg.width}x{cfg.height} frames of {cfg.name} ({rays} rays, {dt:.1f} s)",
-            "ms_per_frame": round(1e3 * dt / frames, 1), "host": host}
+
+    def sample(threads, secs):
+        acc = np.zeros((cfg.height, cfg.width, 4), np.float32)
+        rays = frames = 0
+        t0 = time.perf_counter()
+        while True:
+            acc, c = orc.render(cfg.width, cfg.height, cfg.integrator, frames, eye, rot, accum=acc,
+                                max_bounce=cfg.max_bounce, threads=threads)
+            rays += c.rays
+            frames += 1
+            if time.perf_counter() - t0 >= secs:
+                break
+        dt = time.perf_counter() - t0
+        return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+                "sample": f"{frames} full {cfg.width}x{cfg.height} frames of {cfg.name} ({rays} rays, {dt:.1f} s)",
+                "ms_per_frame": round(1e3 * dt / frames, 1)}
+
+    out = {**sample(cores, seconds), "host": host}
+    # the CPU tracer on all host cores of the box too (nproc threads, however many
+    # of them the job's CPU share actually runs), beside the per-GPU share above
+    if all_seconds > 0 and host["nproc"] > cores:
+        out["all_cores"] = sample(host["nproc"], all_seconds)
+    return out
 
 
 def host_cpu():
@@ -368,8 +406,14 @@ def host_cpu():
                 break
     except OSError:
         pass
+    quota = None  # the job's CPU bandwidth limit (cgroup v2 cpu.max: quota/period CPUs), if any
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return {"threads": max(1, threads), "nproc": nproc, "affinity": affinity,
-            "omp_num_threads": share or None, "cpu_model": model}
+            "omp_num_threads": share or None, "cgroup_cpus": quota, "cpu_model": model}
 
 
 if __name__ == "__main__":

@@ -34,6 +34,12 @@ namespace pt {
 constexpr int REGEN_LDS_STACK = PT_REGEN_LDS_STACK;
 // minimum waves per SIMD the register allocator must allow (uniform integrators
 // fit 128 VGPRs without spilling; the MIS state machine does not)
+// Dynamic ray fetch for the 4-wide walk (pt_trace.h walk4Run): a wave stops walking as soon
+// as this many of its walking lanes are done, and those lanes shade and take their next ray
+// while the others resume their walks (0 = every walk runs to its end first, traceRay4).
+#ifndef PT_REGEN_YIELD
+#define PT_REGEN_YIELD 0
+#endif
 #ifndef PT_REGEN_MIN_WAVES_U
 #define PT_REGEN_MIN_WAVES_U 4
 #endif
@@ -257,6 +263,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   int tile = -1;      // current 8x8 wave tile (wave-uniform)
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
   bool active = false;
+  bool walking = false;  // PT_REGEN_YIELD: the lane's ray has a walk in progress (w, st)
+  Walk4 w;
   PathState s;
   s.px = s.py = 0;
   s.kind = K_NONE;
@@ -303,7 +311,22 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
     if (!active) continue;
     float t;
     int tri;
-    if (W4 && p.scene.fast) {
+    if (PT_REGEN_YIELD > 0 && W4 && p.scene.fast) {
+      if (!walking) {
+        walk4Begin(p.scene, w, st, C);
+        walking = true;
+      }
+      walk4Run<CULL, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(p.scene, s.o, s.d, s.kind == K_SHADOW, w, st,
+                                                                       top, PT_REGEN_YIELD);
+      if (!walk4Done(w)) continue;  // stopped for the lanes that are done: resumes next iteration
+      walking = false;
+      t = w.tbest;
+      tri = w.best >= 0 ? p.scene.fastTri[w.best] : -1;
+      if (w.tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t))) {
+        C.rays--;  // the same ray, counted once
+        tri = traceRay<false, CULL, false>(p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW);
+      }
+    } else if (W4 && p.scene.fast) {
       bool tie = false;
       const int pos = traceRay4<CULL, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(p.scene, s.o, s.d, t, st, C,
                                                                                       s.kind == K_SHADOW, top, &tie);

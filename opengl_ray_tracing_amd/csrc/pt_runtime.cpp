@@ -140,6 +140,7 @@ struct pt_ctx {
   bool pipe = false;                        // this context pipelines its megakernel frames
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
   bool gridShare = true;                    // frames in flight split the persistent grid (PT_GRID_SHARE=0: not)
+  int gridPct = 100;                        // % of residency the frames in flight split (PT_GRID_PCT)
   hipStream_t slotStream[PIPE] = {};
   hipEvent_t kernelDone[PIPE] = {};         // slot's last frame kernel (+ reorder) ended
   bool slotBusy[PIPE] = {};                 // kernelDone[k] has been recorded since the last sync
@@ -332,6 +333,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     ctx->pipeDepth = std::min(ctx->pipeDepth, std::max(2, hwq - 2));
     if (const char* e = std::getenv("PT_PIPE_DEPTH")) ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
     // slot streams are created as a depth first uses them (ensureSlots): streams beyond the
     // hardware queues share queues, which serialises their work
     for (int k = 0; k < COLS; k++) CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
@@ -1622,7 +1624,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     for (int k = 0; k < D && !others; k++)
       others = k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
     (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
-    if (others) grid = std::max(NUM_QUEUES, fullGrid / D);
+    if (others) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * ctx->gridPct / (100 * D)));
   }
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)fullGrid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);

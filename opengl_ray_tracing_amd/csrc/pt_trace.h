@@ -504,6 +504,123 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
   return best;
 }
 
+// ----------------------------------------------------------------- resumable 4-wide walk
+// traceRay4 as a walk that can stop and resume (the regen kernel's dynamic ray
+// fetch, PT_REGEN_YIELD): the walk's state is a Walk4 plus the lane's stack, and
+// walk4Run returns once the lane's walk is done -- or, for the whole wave, as
+// soon as `yield` of the lanes walking with it are done, so that those lanes go
+// on with their paths (shade, take the next ray or pixel) instead of idling
+// until the wave's longest walk ends; the others resume where they stopped on
+// the next call. Per ray the sequence of node visits, leaf tests and closest-hit
+// updates is traceRay4's (stopping between outer iterations changes nothing a
+// lane computes), so results are identical.
+struct Walk4 {
+  float tbest;
+  int best;
+  int ref;   // next item in visiting order (REF_NONE: none)
+  int leaf;  // parked leaf (REF_NONE: none)
+  bool tie;
+};
+__device__ __forceinline__ bool walk4Done(const Walk4& w) { return w.ref == REF_NONE && w.leaf == REF_NONE; }
+template <class StackType>
+__device__ __forceinline__ void walk4Begin(const SceneView& S, Walk4& w, StackType& st, Counters& C) {
+  w.tbest = PT_INF;
+  w.best = -1;
+  w.ref = S.f4Root;
+  w.leaf = REF_NONE;
+  w.tie = false;
+  st.reset();
+  C.rays++;
+}
+template <bool CULL, class StackType, bool LDSTOP>
+__device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool anyRT, Walk4& w, StackType& st,
+                                         const float4* top, int yield) {
+  const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const FusedRay fr = fusedRay(o, inv);
+  const f32x2 ix = {fr.inv.x, fr.inv.x}, iy = {fr.inv.y, fr.inv.y}, iz = {fr.inv.z, fr.inv.z};
+  const f32x2 ox = {fr.noi.x, fr.noi.x}, oy = {fr.noi.y, fr.noi.y}, oz = {fr.noi.z, fr.noi.z};
+  while (true) {
+    const bool done = walk4Done(w);
+    if (__ballot(!done) == 0 || __popcll(__ballot(done)) >= yield) break;  // wave-uniform
+    if (done) continue;
+    while (w.ref >= 0) {
+      const float4* nd = S.fbvh4 + (size_t)W4_F4 * w.ref;
+      if (LDSTOP && w.ref < S.f4nTop) nd = top + W4_F4 * w.ref;
+      const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+      float key[4];
+      int r[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+      const float lim = w.tbest + 1e-3f * fmaxf(1.0f, w.tbest);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const f32x2 Lx = h ? f32x2{lx.z, lx.w} : f32x2{lx.x, lx.y}, Ly = h ? f32x2{ly.z, ly.w} : f32x2{ly.x, ly.y};
+        const f32x2 Lz = h ? f32x2{lz.z, lz.w} : f32x2{lz.x, lz.y}, Hx = h ? f32x2{hx.z, hx.w} : f32x2{hx.x, hx.y};
+        const f32x2 Hy = h ? f32x2{hy.z, hy.w} : f32x2{hy.x, hy.y}, Hz = h ? f32x2{hz.z, hz.w} : f32x2{hz.x, hz.y};
+        const f32x2 fx = __builtin_elementwise_fma(Hx, ix, ox), fy = __builtin_elementwise_fma(Hy, iy, oy),
+                    fz = __builtin_elementwise_fma(Hz, iz, oz);
+        const f32x2 nx = __builtin_elementwise_fma(Lx, ix, ox), ny = __builtin_elementwise_fma(Ly, iy, oy),
+                    nz = __builtin_elementwise_fma(Lz, iz, oz);
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int c = 2 * h + e;
+          const float t1 = fminf(fmaxf(fx[e], nx[e]), fminf(fmaxf(fy[e], ny[e]), fmaxf(fz[e], nz[e])));
+          const float t0 = fmaxf(fminf(fx[e], nx[e]), fmaxf(fminf(fy[e], ny[e]), fminf(fz[e], nz[e])));
+          bool hit = r[c] != REF_NONE && t1 >= t0 && t1 > 0.0f;
+          if (CULL) hit = hit && !(t0 > lim);
+          key[c] = hit ? t0 : PT_INF_KEY;
+        }
+      }
+      cswap(key[0], r[0], key[1], r[1]);
+      cswap(key[2], r[2], key[3], r[3]);
+      cswap(key[0], r[0], key[2], r[2]);
+      cswap(key[1], r[1], key[3], r[3]);
+      cswap(key[1], r[1], key[2], r[2]);
+      int next;
+      if (key[0] < PT_INF_KEY) {
+        if (key[3] < PT_INF_KEY) st.push(r[3]);
+        if (key[2] < PT_INF_KEY) st.push(r[2]);
+        if (key[1] < PT_INF_KEY) st.push(r[1]);
+        next = r[0];
+      } else {
+        next = st.sp > 0 ? st.pop() : REF_NONE;
+      }
+      if (isLeafRef(next) && w.leaf == REF_NONE) {
+        w.leaf = next;
+        next = st.sp > 0 ? st.pop() : REF_NONE;
+      }
+      w.ref = next;
+      if (__ballot(w.leaf == REF_NONE) == 0) break;
+    }
+    if (w.leaf == REF_NONE && isLeafRef(w.ref)) {
+      w.leaf = w.ref;
+      w.ref = st.sp > 0 ? st.pop() : REF_NONE;
+    }
+    if (w.leaf == REF_NONE) continue;  // w.ref == REF_NONE too: this lane's walk is done
+    const uint32_t v = ~(uint32_t)w.leaf;
+    const int start = (int)(v >> LEAF_CNT_BITS);
+    const int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
+    w.leaf = REF_NONE;
+    for (int k = 0; k < cnt; k += 2) {
+      const int i = start + k;
+      const bool second = k + 1 < cnt;
+      float t0, t1;
+      bool g0, g1;
+      pairTest(S.fpairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1);
+      if (g0 && t0 == w.tbest) w.tie = true;
+      if (g0 && t0 < w.tbest) {
+        w.tbest = t0;
+        w.best = i;
+        if (anyRT) { w.ref = REF_NONE; break; }  // any hit: the walk ends here (traceRay4's return)
+      }
+      if (g1 && second && t1 == w.tbest) w.tie = true;
+      if (g1 && second && t1 < w.tbest) {
+        w.tbest = t1;
+        w.best = i + 1;
+        if (anyRT) { w.ref = REF_NONE; break; }
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------- reference-exact results
 // Reference-exact results through the runtime's tree. The reference's closest
 // hit is the first, in its traversal order, of the triangles with the least t

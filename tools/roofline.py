@@ -35,7 +35,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "gpurun_out"
-PROBE = 20
+PROBE = 90  # bench.py PROBE_FRAMES: policy-probe frames ahead of the warmup and timed frames
 TRACE_RUN = (5, 30)    # tools/gpu_profile.sh: --warmup 5 --steps 30 under --kernel-trace
 COUNTER_RUN = (2, 10)  # --warmup 2 --steps 10 under each --pmc pass
 BENCH_KERNEL = re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true(, \d+)?(, (true|false))?>")
@@ -98,27 +98,45 @@ def main():
                 for r in by_disp[di]:
                     vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
                     rows_out.append({"pass": name, **r})
+                r0 = by_disp[di][0]
+                if name == "sq" and r0.get("End_Timestamp"):  # the counter pass's own dispatch duration
+                    vals["_counter_dispatch_ms"].append((int(r0["End_Timestamp"]) - int(r0["Start_Timestamp"])) / 1e6)
         with open(d / "counters.csv", "w", newline="") as fh:
             wr = csv.DictWriter(fh, fieldnames=["pass"] + header)
             wr.writeheader()
             wr.writerows(rows_out)
         m = {k: sum(v) / len(v) for k, v in vals.items()}
         g = lambda k: m.get(k, float("nan"))  # noqa: E731
+        cms = m.pop("_counter_dispatch_ms", float("nan"))
+        vals.pop("_counter_dispatch_ms", None)
+        # the kernel with nothing overlapping it: the serial-frames trace (PT_FLAG_SERIAL_FRAMES)
+        serial_ms = None
+        sp = sorted(glob.glob(f"{prof}/serial/**/run_kernel_trace.csv", recursive=True))
+        if sp:
+            st = [r for r in csv.DictReader(open(sp[0])) if BENCH_KERNEL.search(r["Kernel_Name"])]
+            ssel, _ = timed(st, TRACE_RUN)
+            sms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in ssel]
+            serial_ms = round(sum(sms) / len(sms), 4)
+            shutil.copy(one(f"{prof}/serial/**/run_kernel_stats.csv"), d / "kernel_stats_serial.csv")
         ent = {
             "kernel": sel[-1]["Kernel_Name"], "kernel_ms": round(kernel_ms, 4),
             "valu_insts": round(g("SQ_INSTS_VALU")),
             "dram_bytes": round((2 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024),
             "l2_hit": round(g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")), 4),
             "valu_lane_util": round(g("SQ_THREAD_CYCLES_VALU") / (64 * g("SQ_ACTIVE_INST_VALU")), 4),
-            "clock_ghz_profiled": round(g("GRBM_GUI_ACTIVE") / 8 / (kernel_ms * 1e-3) / 1e9, 3),
+            # GRBM_GUI_ACTIVE summed over the 8 XCDs, over the counter pass's own (serialised)
+            # dispatch durations -- the interval the counters describe
+            "counter_dispatch_ms": round(cms, 4),
+            "clock_ghz_profiled": round(g("GRBM_GUI_ACTIVE") / 8 / (cms * 1e-3) / 1e9, 3),
+            "serial_kernel_ms": serial_ms,
             "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())},
             "samples": {k: len(v) for k, v in sorted(vals.items())},
             "derivation": "valu_insts = SQ_INSTS_VALU; dram_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024; "
                           "per launch, averaged over the bench kernel's timed dispatches of each pass",
         }
         summary[c] = ent
-        print(c, json.dumps({k: ent[k] for k in ("kernel_ms", "valu_insts", "dram_bytes", "l2_hit",
-                                                  "valu_lane_util", "clock_ghz_profiled")}))
+        print(c, json.dumps({k: ent[k] for k in ("kernel_ms", "serial_kernel_ms", "counter_dispatch_ms", "valu_insts",
+                                                  "dram_bytes", "l2_hit", "valu_lane_util", "clock_ghz_profiled")}))
         restate(dst / f"bench_{c}.json", ent)
     cpath.write_text(json.dumps(summary, indent=1) + "\n")
 
@@ -147,7 +165,7 @@ def restate(path: Path, ent: dict):
     bound = max(cand, key=lambda k: cand[k]["frac"])
     rf.update({"bound": bound, **{k: cand[bound][k] for k in ("achieved", "peak", "unit", "frac")},
                "traffic": ent["dram_bytes"], "candidates": cand,
-               "counters": {"source": "profiles/r2/counters.json", "valu_insts_per_launch": ent["valu_insts"],
+               "counters": {"source": f"profiles/{path.parent.name}/counters.json", "valu_insts_per_launch": ent["valu_insts"],
                             "dram_bytes_per_launch": ent["dram_bytes"], "l2_hit": ent["l2_hit"],
                             "profiled_kernel_ms": ent["kernel_ms"]},
                "restated_from_counters_of_this_run": True})
