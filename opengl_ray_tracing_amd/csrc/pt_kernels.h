@@ -32,6 +32,9 @@ constexpr int WIDE_WAVES = 3;
 // (c5: 16 bounces) a lane that takes a new pixel when its path ends beats the
 // lock-step megakernel, whose waves last as long as their longest path (c5: 10.0
 // -> 9.2 ms; on the L2-resident c4 the regen kernel is 3.6x slower)
+#ifndef PT_REGEN_YIELD_REL
+#define PT_REGEN_YIELD_REL 0  // 1: PT_REGEN_YIELD counts 64ths of the lanes walking together, not lanes
+#endif
 #ifndef PT_WIDE_REGEN_WAVES
 #define PT_WIDE_REGEN_WAVES 4
 #endif
@@ -158,6 +161,23 @@ struct Env {
   int w, h, res;        // res = hdrResolution
 };
 
+// Frames in flight sharing work (pt_runtime.cpp "frames in flight"): what differs from
+// one pipelined megakernel frame to the next while scene, env, camera and policies stay
+// the same. frameVarKernel publishes a frame's FrameVar in its slot (frameVars[slot], then
+// frameReady[slot] = the frame's sequence number) right before the frame's kernel; a wave
+// of an earlier frame in flight whose own items are exhausted reads it and takes that
+// frame's items (renderKernel) instead of idling through its own frame's tail.
+struct FrameVar {
+  float4* col;
+  int* queue;
+  const int* tileOrder;
+  int* tileCost;
+  int* tileCostMax;
+  int2* primHit;
+  uint32_t sampleIndex;
+  uint32_t epoch;  // generation of everything else (scene, env, camera, tree, packets, bins)
+};
+
 struct RenderParams {
   SceneView scene;
   Env env;
@@ -205,6 +225,13 @@ struct RenderParams {
   int* tileCost;        // per tile: summed cost of its items this frame (shader cycles), null = not recorded
   int* tileCostMax;     // per tile: its longest item this frame
   unsigned long long* waveTrace;  // PT_WAVE_TRACE builds only: 6 u64 per wave (pt_runtime.cpp, tools/wave_trace.py)
+  // work sharing between frames in flight (FrameVar): null = this frame takes no other frame's items
+  FrameVar* frameVars;   // per slot
+  unsigned* frameReady;  // per slot: sequence number of the frame whose FrameVar is published there
+  uint32_t seq;          // this frame's sequence number
+  int depth;             // slots (frames in flight)
+  int shareAhead;        // most frames ahead of its own whose items a wave takes
+  uint32_t epoch;        // FrameVar::epoch of this frame
 };
 
 struct TraceParams {
@@ -327,5 +354,7 @@ hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed,
 // the running-mean update of a pipelined frame over the rank's owned pixels (PackParams
 // mapping): accum = mix(accum, col, 1 / (frameCounter + 1)) (IS:868-871, pass2.fsh:15)
 hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s);
+// publish a frame's FrameVar in its slot (dst), then ready = seq (RenderParams::frameVars)
+hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, unsigned* ready, uint32_t seq, hipStream_t s);
 
 }  // namespace pt

@@ -268,9 +268,9 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
 // main IS:844-872 for one pixel (px, py from the bottom-left), in two parts:
 // the camera ray (cameraRay + primaryPixel) and the rest of the path
 // (finishPixel, which recomputes the camera ray and RNG state from the pixel).
-__device__ __forceinline__ V3 cameraRay(const RenderParams& p, int px, int py, uint32_t& seed) {
+__device__ __forceinline__ V3 cameraRay(const RenderParams& p, uint32_t sampleIndex, int px, int py, uint32_t& seed) {
   const int W = p.width, H = p.height;
-  seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + p.sampleIndex * 26699u) | 1u;
+  seed = ((uint32_t)px * 1973u + (uint32_t)py * 9277u + sampleIndex * 26699u) | 1u;
   float pixx = (float)(2 * px + 1) / (float)W - 1.0f;
   float pixy = (float)(2 * py + 1) / (float)H - 1.0f;
   float ax = (randf(seed) - 0.5f) / (float)W;
@@ -282,9 +282,12 @@ __device__ __forceinline__ V3 cameraRay(const RenderParams& p, int px, int py, u
   return normalize(dir);
 }
 
-__device__ __forceinline__ void accumulate(const RenderParams& p, int px, int py, V3 color, Counters& C, bool count) {
-  if (!count && p.col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in order
-    stStream(p.col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
+// f: the frame the pixel belongs to (its sample index and colour buffer; FrameVar)
+__device__ __forceinline__ void accumulate(const RenderParams& p, const FrameVar& f, int px, int py, V3 color, Counters& C,
+                                           bool count) {
+  float4* col = f.col;
+  if (!count && col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in order
+    stStream(col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
     return;
   }
   float4* a = p.accum + (size_t)py * p.width + px;
@@ -296,17 +299,17 @@ __device__ __forceinline__ void accumulate(const RenderParams& p, int px, int py
 
 // the camera ray's closest hit; a miss is finished here (sky colour accumulated)
 template <bool CULL, bool COUNT>
-__device__ __forceinline__ int primaryPixel(const RenderParams& p, int px, int py, Stack& st, Counters& C,
-                                            const float4* top, float& t) {
+__device__ __forceinline__ int primaryPixel(const RenderParams& p, const FrameVar& f, int px, int py, Stack& st,
+                                            Counters& C, const float4* top, float& t) {
   uint32_t seed;
-  const V3 dir = cameraRay(p, px, py, seed);
+  const V3 dir = cameraRay(p, f.sampleIndex, px, py, seed);
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
   Tracer<CULL, COUNT> tr{p.scene, st, C, top};
   const int tri = tr.trace(eye, dir, t);
   if (tri < 0) {
     const V3 color = sampleHdr(p.env, dir);
     if (COUNT) C.texels++;
-    accumulate(p, px, py, color, C, COUNT);
+    accumulate(p, f, px, py, color, C, COUNT);
   }
   return tri;
 }
@@ -315,10 +318,10 @@ __device__ __forceinline__ int primaryPixel(const RenderParams& p, int px, int p
 // one packet (tracePacket); a ray that met an exact tie is retraced in the
 // reference order. All 64 lanes call it; valid marks the lanes with a pixel.
 template <bool CULL>
-__device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int py, bool valid, Stack& st, Counters& C,
-                                             const float4* top, PacketEntry* pstack, float& t) {
+__device__ __forceinline__ int primaryPacket(const RenderParams& p, const FrameVar& f, int px, int py, bool valid,
+                                             Stack& st, Counters& C, const float4* top, PacketEntry* pstack, float& t) {
   uint32_t seed;
-  const V3 dir = cameraRay(p, valid ? px : 0, valid ? py : 0, seed);
+  const V3 dir = cameraRay(p, f.sampleIndex, valid ? px : 0, valid ? py : 0, seed);
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
   bool tie;
   int tri;
@@ -401,7 +404,7 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, int px, int 
   }
   if (valid && tri < 0) {
     const V3 color = sampleHdr(p.env, dir);
-    accumulate(p, px, py, color, C, false);
+    accumulate(p, f, px, py, color, C, false);
   }
   return tri;
 }
@@ -433,6 +436,8 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   }
   const int n = b1 - b0;
   int2* out = p.primHit + (size_t)py * p.width + px;
+  FrameVar fp{};  // this launch's frame (accumulate's colour buffer)
+  fp.col = p.col;
   if (n > PT_PASS_BIN_CAP) {  // the frame kernel traces this tile's camera rays (the megakernel as a packet)
     if (valid) *out = make_int2(PRIM_TILE, 0);
     return;
@@ -444,7 +449,7 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   }
   __syncthreads();
   uint32_t seed;
-  const V3 dir = cameraRay(p, valid ? px : 0, valid ? py : 0, seed);
+  const V3 dir = cameraRay(p, p.sampleIndex, valid ? px : 0, valid ? py : 0, seed);
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
   float tbest = PT_INF;
   int best = -1;
@@ -468,7 +473,7 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
       rays = 1;
       if (res == PRIM_MISS) {
         Counters C = {0, 0, 0, 0, 0};
-        accumulate(p, px, py, sampleHdr(p.env, dir), C, false);
+        accumulate(p, fp, px, py, sampleHdr(p.env, dir), C, false);
       }
     }
     *out = make_int2(res, __float_as_int(tbest));
@@ -484,19 +489,20 @@ hipError_t launchPrimary(const RenderParams& p, hipStream_t s) {
 
 // the rest of the path of a pixel whose camera ray hit triangle tri at t
 template <int INTEG, bool CULL, bool COUNT>
-__device__ __forceinline__ void finishPixel(const RenderParams& p, int px, int py, int tri, float t, Stack& st,
-                                            Counters& C, const float4* top) {
+__device__ __forceinline__ void finishPixel(const RenderParams& p, const FrameVar& f, int px, int py, int tri, float t,
+                                            Stack& st, Counters& C, const float4* top) {
   Tracer<CULL, COUNT> tr{p.scene, st, C, top};
   uint32_t seed;
-  const V3 dir = cameraRay(p, px, py, seed);  // the same ray and RNG state as primaryPixel
+  const uint32_t sampleIndex = f.sampleIndex;
+  const V3 dir = cameraRay(p, sampleIndex, px, py, seed);  // the same ray and RNG state as primaryPixel
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
   Hit first;
   finishHit(p.scene, tri, eye, dir, t, first);
   V3 Li;
   if (INTEG == 0) Li = pathLambert(tr, p.env, first, p.maxBounce, seed, C, COUNT);
   else if (INTEG == 1) Li = pathDisneyUniform(tr, p.env, first, p.maxBounce, seed, C, COUNT);
-  else Li = pathMIS(tr, p.env, first, p.maxBounce, seed, px, py, p.sampleIndex, C, COUNT);
-  accumulate(p, px, py, first.m.emissive + Li, C, COUNT);
+  else Li = pathMIS(tr, p.env, first, p.maxBounce, seed, px, py, sampleIndex, C, COUNT);
+  accumulate(p, f, px, py, first.m.emissive + Li, C, COUNT);
 }
 
 // ------------------------------------------------ BASIC (BasicRayTracingWithC++)
@@ -895,8 +901,22 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   // 0.59 -- the coherence of one tile's rays is worth more than full lanes.)
   const int waveId = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6), numWaves = gridDim.x * (BLOCK / 64);
   int dealt = 0;  // statically dealt items taken (band order)
+  // fv: the frame whose items this wave takes -- this launch's own frame, then (work
+  // sharing, RenderParams::frameVars) the next frames in flight. Kept in the wave's LDS
+  // slot and read where used, so none of it is live in registers across a path.
+  __shared__ FrameVar s_fv[BLOCK / 64];
+  FrameVar& fv = s_fv[threadIdx.x >> 6];
+  fv.col = p.col;  // every lane stores the same values (a wave's LDS accesses are in order)
+  fv.queue = p.queue;
+  fv.tileOrder = p.tileOrder;
+  fv.tileCost = p.tileCost;
+  fv.tileCostMax = p.tileCostMax;
+  fv.primHit = p.primHit;
+  fv.sampleIndex = p.sampleIndex;
+  int ahead = 0;         // frames ahead of this launch's own frame
+  uint32_t shared = 0;   // items this wave took from later frames (pt_frame_stats.shared_items)
   auto claim = [&]() -> int {
-    if (p.staticItems > 0) {
+    if (p.staticItems > 0) {  // (frames dealing items statically share no work)
       const int t = waveId + dealt * numWaves;
       if (t < p.staticItems) {
         dealt++;
@@ -905,12 +925,44 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
       const int it = cur.next(p.queue, p.dynPerQueue, p.numItems - p.staticItems, home);
       return it < 0 ? it : p.staticItems + it;
     }
-    return cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+    return cur.next(fv.queue, p.perQueue, p.numItems, home, fv.tileOrder, p.orderCap);
+  };
+  // the next frame in flight whose FrameVar is published (same epoch): its items are taken next
+  auto nextFrame = [&]() -> bool {
+    if (COUNT || !p.frameVars || ++ahead > p.shareAhead) return false;
+    const uint32_t want = p.seq + (uint32_t)ahead;
+    const int slot = (int)(want % (uint32_t)p.depth);
+    if (__hip_atomic_load(p.frameReady + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) return false;
+    const FrameVar* v = p.frameVars + slot;
+    // wave-uniform values: kept in scalar registers
+    auto ld32 = [](const uint32_t* a) {
+      return (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    auto ld64 = [&](void* const* a) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(a);
+      return (void*)((unsigned long long)ld32(w) | (unsigned long long)ld32(w + 1) << 32);
+    };
+    if (ld32(&v->epoch) != p.epoch) return false;
+    fv.col = (float4*)ld64((void* const*)&v->col);
+    fv.queue = (int*)ld64((void* const*)&v->queue);
+    fv.tileOrder = (const int*)ld64((void* const*)&v->tileOrder);
+    fv.tileCost = (int*)ld64((void* const*)&v->tileCost);
+    fv.tileCostMax = (int*)ld64((void* const*)&v->tileCostMax);
+    fv.primHit = (int2*)ld64((void* const*)&v->primHit);
+    fv.sampleIndex = ld32(&v->sampleIndex);
+    cur = TileCursor();
+    return true;
   };
   int item = claim();
-  while (item >= 0) {
+  while (true) {
+    if (item < 0) {
+      if (!nextFrame()) break;
+      item = claim();
+      continue;
+    }
+    if (!COUNT && ahead > 0) shared++;
 #if PT_CLAIM_AHEAD
-    cur.claimAhead(p.queue, home);
+    cur.claimAhead(fv.queue, home);
 #endif
     const int w = itemTile(item);
     const long long t0 = COUNT ? 0 : clock64();
@@ -927,33 +979,40 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     const int px = gx * p.shardSize + (s % sub) * 8 + (k & 7);
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
     const bool valid = lane < nLanes && px < p.width && py < p.height;
-    if (!COUNT && p.primHit) {  // camera rays already traced by primaryKernel
-      const int2 h = valid ? p.primHit[(size_t)py * p.width + px] : make_int2(PRIM_MISS, 0);
+    int2* const primHit = fv.primHit;
+    if (!COUNT && primHit) {  // camera rays already traced by primaryKernel
+      int2 h = make_int2(PRIM_MISS, 0);
+      if (valid) {  // through L2: another frame in flight's results may be read here (work sharing)
+        const unsigned long long b = __hip_atomic_load(
+            reinterpret_cast<const unsigned long long*>(primHit + (size_t)py * p.width + px), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        h = make_int2((int)(uint32_t)b, (int)(uint32_t)(b >> 32));
+      }
       int tri = h.x;
       float t = __int_as_float(h.y);
       if (__ballot(valid && tri == PRIM_TILE)) {  // wave-uniform: the whole tile
-        tri = primaryPacket<CULL>(p, px, py, valid, st, C, top, pstack, t);
+        tri = primaryPacket<CULL>(p, fv, px, py, valid, st, C, top, pstack, t);
       } else if (valid && tri == PRIM_RETRACE) {  // in the reference order, as primaryPacket does
         uint32_t seed;
-        const V3 dir = cameraRay(p, px, py, seed);
+        const V3 dir = cameraRay(p, fv.sampleIndex, px, py, seed);
         const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
         tri = traceRay<false, CULL, false, Stack>(p.scene, eye, dir, t, st, C);
-        if (tri < 0) accumulate(p, px, py, sampleHdr(p.env, dir), C, false);
+        if (tri < 0) accumulate(p, fv, px, py, sampleHdr(p.env, dir), C, false);
       }
-      if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);
+      if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, fv, px, py, tri, t, st, C, top);
     } else if (!COUNT && (p.packets || p.binStart)) {
       float t;
-      const int tri = primaryPacket<CULL>(p, px, py, valid, st, C, top, pstack, t);
-      if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);
+      const int tri = primaryPacket<CULL>(p, fv, px, py, valid, st, C, top, pstack, t);
+      if (valid && tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, fv, px, py, tri, t, st, C, top);
     } else if (valid) {
       float t;
-      const int tri = primaryPixel<CULL, COUNT>(p, px, py, st, C, top, t);
-      if (tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, px, py, tri, t, st, C, top);
+      const int tri = primaryPixel<CULL, COUNT>(p, fv, px, py, st, C, top, t);
+      if (tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, fv, px, py, tri, t, st, C, top);
     }
-    if (!COUNT && p.tileCost && lane == 0) {
+    if (!COUNT && lane == 0 && fv.tileCost) {
       const int dt = (int)min(clock64() - t0, (long long)0x3fffffff);
-      atomicAdd(p.tileCost + w, dt);
-      atomicMax(p.tileCostMax + w, dt);
+      atomicAdd(fv.tileCost + w, dt);
+      atomicMax(fv.tileCostMax + w, dt);
     }
 #if PT_WAVE_TRACE
     const unsigned long long tEnd = wall_clock64();
@@ -972,7 +1031,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     }
 #endif
 #if PT_CLAIM_AHEAD
-    item = cur.nextAhead(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
+    item = cur.nextAhead(fv.queue, p.perQueue, p.numItems, home, fv.tileOrder, p.orderCap);
 #else
     item = claim();
 #endif
@@ -985,6 +1044,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   }
 #endif
   addRays(p.rayShards, C.rays);
+  if (!COUNT && shared && lane == 0)
+    atomicAdd(reinterpret_cast<unsigned long long*>(p.stats + 5), (unsigned long long)shared);
   if (COUNT) {
     uint32_t n = waveSum(C.nodes), t = waveSum(C.tris), m = waveSum(C.mats), x = waveSum(C.texels);
     if (lane == 0) {
@@ -1177,6 +1238,14 @@ hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint
     return v == 64 || v == 128 || v == 256 || v == 512 || v == 1024 ? v : 256;
   }();
   hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + bs - 1) / bs)), dim3(bs), 0, s, p, accum, col, frameCounter);
+  return hipGetLastError();
+}
+__global__ void frameVarKernel(FrameVar v, FrameVar* dst, unsigned* ready, uint32_t seq) {
+  *dst = v;
+  __hip_atomic_store(ready, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // after the FrameVar
+}
+hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, unsigned* ready, uint32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(frameVarKernel, dim3(1), dim3(1), 0, s, v, dst, ready, seq);
   return hipGetLastError();
 }
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s) {

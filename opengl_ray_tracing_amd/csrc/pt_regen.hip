@@ -38,7 +38,7 @@ constexpr int REGEN_LDS_STACK = PT_REGEN_LDS_STACK;
 // as this many of its walking lanes are done, and those lanes shade and take their next ray
 // while the others resume their walks (0 = every walk runs to its end first, traceRay4).
 #ifndef PT_REGEN_YIELD
-#define PT_REGEN_YIELD 0
+#define PT_REGEN_YIELD 40  // c5: 0 (off) 6.97 ms, 8 6.98, 16 6.59, 32 5.78, 40 5.64, 48 5.63-5.71, 56 5.85, 60 6.17
 #endif
 #ifndef PT_REGEN_MIN_WAVES_U
 #define PT_REGEN_MIN_WAVES_U 4

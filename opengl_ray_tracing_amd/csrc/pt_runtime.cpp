@@ -141,6 +141,15 @@ struct pt_ctx {
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
   bool gridShare = true;                    // frames in flight split the persistent grid (PT_GRID_SHARE=0: not)
   int gridPct = 100;                        // % of residency the frames in flight split (PT_GRID_PCT)
+  // work sharing between frames in flight (renderKernel, FrameVar; PT_SHARE_WORK=1: on)
+  bool shareWork = false;
+  // frames ahead of its own whose items a wave may take (PT_SHARE_AHEAD): a kernel lasts until
+  // the last of them is claimed out, and its slot's next frame cannot start before it ends
+  int shareAhead = 1;
+  FrameVar* d_frameVars = nullptr;          // per slot
+  unsigned* d_frameReady = nullptr;         // per slot: sequence number of the published frame
+  uint32_t shareEpoch = 0;                  // FrameVar::epoch: bumped when anything else a frame reads changes
+  unsigned long long shareKey[3] = {~0ull, ~0ull, ~0ull};  // what the epoch was issued for (renderOne)
   hipStream_t slotStream[PIPE] = {};
   hipEvent_t kernelDone[PIPE] = {};         // slot's last frame kernel (+ reorder) ended
   bool slotBusy[PIPE] = {};                 // kernelDone[k] has been recorded since the last sync
@@ -334,6 +343,13 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     if (const char* e = std::getenv("PT_PIPE_DEPTH")) ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
+    if (const char* e = std::getenv("PT_SHARE_WORK")) ctx->shareWork = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PT_SHARE_AHEAD")) ctx->shareAhead = std::max(1, std::atoi(e));
+    // work sharing between frames in flight (renderKernel, FrameVar): per slot the published
+    // frame variables and the sequence number of the frame they belong to (none yet: ~0)
+    CKC(hipMalloc(&ctx->d_frameVars, PIPE * sizeof(FrameVar)));
+    CKC(hipMalloc(&ctx->d_frameReady, PIPE * sizeof(unsigned)));
+    CKC(hipMemset(ctx->d_frameReady, 0xff, PIPE * sizeof(unsigned)));
     // slot streams are created as a depth first uses them (ensureSlots): streams beyond the
     // hardware queues share queues, which serialises their work
     for (int k = 0; k < COLS; k++) CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
@@ -402,6 +418,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
+  dfree(ctx->d_frameVars); dfree(ctx->d_frameReady);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
   freePrimaryBins(ctx->bins);
   for (int k = 0; k < PIPE; k++) {
@@ -1631,6 +1648,11 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (rc) return rc;
   const size_t npix = (size_t)c.width * c.height;
   if (piped && !ctx->d_col[colIdx]) CK(hipMalloc(&ctx->d_col[colIdx], npix * sizeof(float4)));
+  // the colour buffer's previous frame (depth + 1 back) has been mixed -- and so, with work
+  // sharing, every frame before it has ended, including any that took this slot's previous
+  // frame's items: only then are the slot's queue counters, order list and camera-ray
+  // results reset for this frame
+  if (piped && ctx->frameNo >= (unsigned long long)(D + 1)) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
   int* queue = reinterpret_cast<int*>(ctx->d_ctl + CTL_QUEUES) + (size_t)slot * NUM_QUEUES * CTL_LINE_INTS;
   CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   RenderParams p;
@@ -1753,8 +1775,34 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (piped && probing) {
     if (int e = waitOthers()) return e;
   }
-  // the colour buffer's previous frame (depth + 1 back) has been mixed
-  if (piped && ctx->frameNo >= (unsigned long long)(D + 1)) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
+  // Work sharing between frames in flight (renderKernel, FrameVar): this frame publishes its
+  // FrameVar so that waves of earlier frames in flight whose own items are exhausted take its
+  // items; and its waves take later frames' items. Not while the policy probe times frames,
+  // nor with statically dealt items. The epoch changes whenever anything else the frame
+  // reads (camera, scene, env, tree, packets, bins) differs from the previous frame's.
+  const bool share = piped && D > 1 && ctx->shareWork && !regen && !probing && p.staticItems == 0;
+  if (share) {
+    unsigned long long h = 1469598103934665603ull;  // FNV-1a of the camera
+    auto mixIn = [&](const void* b, size_t n) {
+      for (size_t i = 0; i < n; i++) h = (h ^ reinterpret_cast<const unsigned char*>(b)[i]) * 1099511628211ull;
+    };
+    mixIn(eye, 3 * sizeof(float));
+    mixIn(cameraRotate, 16 * sizeof(float));
+    const unsigned long long key[3] = {
+        h, (unsigned long long)(p.scene.fast | p.packets << 1 | (p.binStart ? 4 : 0) | (p.primHit ? 8 : 0)) |
+               (unsigned long long)ctx->sceneVersion << 8 | (unsigned long long)ctx->policyKey << 36,
+        (unsigned long long)ctx->binGen};
+    if (std::memcmp(key, ctx->shareKey, sizeof(key))) {
+      ctx->shareEpoch++;
+      std::memcpy(ctx->shareKey, key, sizeof(key));
+    }
+    p.frameVars = ctx->d_frameVars;
+    p.frameReady = ctx->d_frameReady;
+    p.seq = (uint32_t)ctx->frameNo;
+    p.depth = D;
+    p.shareAhead = std::min(ctx->shareAhead, D - 1);
+    p.epoch = ctx->shareEpoch;
+  }
   int erc = launchEvents(ctx, &evb, &eve);
   if (erc) return erc;
 #if PT_WAVE_TRACE
@@ -1771,8 +1819,28 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
 #endif
   CK(hipEventRecord(evb, S));
   if (p.primHit) CK(launchPrimary(p, S));
+  if (share) {
+    FrameVar fv;
+    fv.col = p.col;
+    fv.queue = p.queue;
+    fv.tileOrder = p.tileOrder;
+    fv.tileCost = p.tileCost;
+    fv.tileCostMax = p.tileCostMax;
+    fv.primHit = p.primHit;
+    fv.sampleIndex = p.sampleIndex;
+    fv.epoch = p.epoch;
+    CK(launchFrameVar(fv, ctx->d_frameVars + slot, ctx->d_frameReady + slot, p.seq, S));
+  }
   if (regen) CK(launchRegen(p, c.integrator, grid, S, cull, wide));
   else CK(launchRender(p, c.integrator, grid, S, cull, count, wide));
+  // With work sharing, waves of earlier frames may still be taking this frame's items after
+  // its own kernel has ended: the frame counts as ended (kernelDone, and before that the
+  // reorder that rewrites this slot's order list) once the previous frame has ended too, so
+  // by induction once every earlier frame has.
+  if (share && ctx->frameNo >= 1) {
+    const int prev = (int)((ctx->frameNo - 1) % (unsigned)D);
+    if (ctx->slotBusy[prev]) CK(hipStreamWaitEvent(S, ctx->kernelDone[prev], 0));
+  }
 #if PT_WAVE_TRACE
   if (dTrace) {
     std::vector<unsigned long long> tr(nTrace);
@@ -2061,6 +2129,7 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
     st->kernel_ms_total = std::max(st->kernel_ms_total, q.kernel_ms_total);
     st->max_stack = std::max(st->max_stack, q.max_stack);
     st->split_items += q.split_items;
+    st->shared_items += q.shared_items;
   }
   st->devices = 1 + (int)ctx->peers.size();
   st->gather = ctx->gather ? ctx->gather->mode : 0;
@@ -2069,7 +2138,7 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
 
 static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   if (int rc = syncStreams(ctx)) return rc;
-  unsigned long long h[5];
+  unsigned long long h[6];
   std::vector<unsigned long long> shards((size_t)RAY_SHARDS * RAY_SHARD_STRIDE);
   CK(hipMemcpy(h, ctx->d_ctl + CTL_STATS, sizeof(h), hipMemcpyDeviceToHost));
   CK(hipMemcpy(shards.data(), ctx->d_ctl + CTL_RAYS, shards.size() * sizeof(unsigned long long),
@@ -2081,6 +2150,7 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->tri_fetch = h[2];
   st->mat_fetch = h[3];
   st->tex_fetch = h[4];
+  st->shared_items = (int)h[5];
   while (foldOne(ctx, true)) {
   }
   st->kernel_ms = ctx->launches > 0 ? ctx->msLast : 0.0f;

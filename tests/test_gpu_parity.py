@@ -290,6 +290,44 @@ def test_pipelined_frames_equal_serial_frames(request, monkeypatch, name, tile, 
     assert sa.rays == sb.rays
 
 
+@pytest.mark.parametrize("name,tile,flags", [("c4", (0, 8), 0), ("c2", (3, 8), 0), ("c2", (0, 1), 0),
+                                              ("c4", (1, 4), "primary")])
+def test_shared_work_frames_equal_serial_frames(request, monkeypatch, name, tile, flags):
+    """Work sharing between frames in flight (renderKernel, FrameVar: waves of an earlier
+    frame's kernel take items of the next frames in flight) gives the images and ray counts
+    of serial frames bit for bit, on small screen-tile shares (where frames end fastest and
+    sharing is most frequent), a whole frame, and with the camera-ray pass (its per-slot
+    results read by other frames' waves); shared_items shows that items were shared."""
+    from opengl_ray_tracing_amd import FLAG_PRIMARY_PASS, FLAG_SERIAL_FRAMES
+    monkeypatch.setenv("PT_PIPE_DEPTH", "8")
+    monkeypatch.setenv("PT_SHARE_WORK", "1")
+    cfg, tris, nodes, hdr = request.getfixturevalue(name)
+    eye, rot = orbit_camera(*cfg.camera)
+    w, h = 960, 540
+    extra = FLAG_PRIMARY_PASS if flags == "primary" else 0
+
+    def run(fl):
+        out = []
+        with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=fl | extra, tile_rank=tile[0],
+                      tile_world=tile[1]) as r:
+            r.upload_scene(tris, nodes)
+            r.upload_env(hdr)
+            for f in range(64):
+                r.render_frame(eye, rot, f, sync=False)
+                if f == 40:
+                    out.append(r.accum())
+            out.append(r.accum())
+            return out, r.stats()
+
+    a, sa = run(0)
+    b, sb = run(FLAG_SERIAL_FRAMES)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert sa.rays == sb.rays
+    assert sb.shared_items == 0
+    assert sa.shared_items > 0, "no items were shared between frames in flight"
+
+
 @pytest.mark.parametrize("name,integrator,tile", [("c2", "lambert", (0, 1)), ("c3", "mis", (0, 1)),
                                                   ("c4", "mis", (0, 1)), ("c2", "lambert", (2, 3))])
 def test_camera_bins_equal_bvh_camera_rays(request, name, integrator, tile):
