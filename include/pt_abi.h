@@ -26,10 +26,9 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 5  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
+#define PT_ABI_VERSION 4  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
                              3: scene-upload fields at the end of pt_frame_stats, pt_build_bvh_device;
-                             4: BASIC shapes as doubles, its double image, the replayed random stream;
-                             5: pt_frame_stats.shared_items */
+                             4: BASIC shapes as doubles, its double image, the replayed random stream */
 
 /* error codes */
 #define PT_OK 0
@@ -127,8 +126,6 @@ typedef struct pt_frame_stats {
   int accel_depth;      /* and its depth (root = 1) */
   int regen;            /* 1: the last frame ran the path-regeneration kernel (PT_FLAG_REGEN, or a large
                            Disney/MIS scene), 0: the lock-step megakernel */
-  int shared_items;     /* megakernel frames in flight: work items of a frame taken by waves of an
-                           earlier frame's kernel (work sharing) since the reset */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;

@@ -13,7 +13,7 @@ from . import _build
 
 _lib = None
 
-ABI_VERSION = 5  # include/pt_abi.h PT_ABI_VERSION
+ABI_VERSION = 4  # include/pt_abi.h PT_ABI_VERSION
 c_float_p = C.POINTER(C.c_float)
 c_double_p = C.POINTER(C.c_double)
 c_int_p = C.POINTER(C.c_int)
@@ -37,7 +37,7 @@ class PtFrameStats(C.Structure):
         ("split_items", C.c_int), ("runtime_tree", C.c_int),
         ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int), ("frames_in_flight", C.c_int),
         ("upload_ms", C.c_float), ("accel_build_ms", C.c_float), ("accel_device", C.c_int),
-        ("accel_nodes", C.c_int), ("accel_depth", C.c_int), ("regen", C.c_int), ("shared_items", C.c_int),
+        ("accel_nodes", C.c_int), ("accel_depth", C.c_int), ("regen", C.c_int),
     ]
 
 

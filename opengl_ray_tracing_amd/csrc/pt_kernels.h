@@ -161,21 +161,13 @@ struct Env {
   int w, h, res;        // res = hdrResolution
 };
 
-// Frames in flight sharing work (pt_runtime.cpp "frames in flight"): what differs from
-// one pipelined megakernel frame to the next while scene, env, camera and policies stay
-// the same. frameVarKernel publishes a frame's FrameVar in its slot (frameVars[slot], then
-// frameReady[slot] = the frame's sequence number) right before the frame's kernel; a wave
-// of an earlier frame in flight whose own items are exhausted reads it and takes that
-// frame's items (renderKernel) instead of idling through its own frame's tail.
+// A pipelined megakernel frame's colour buffer and running-mean weight, published in its slot
+// (frameVarKernel, before the frame's kernel) for the waves of earlier frames' kernels that
+// mix its tiles into the accumulation (renderKernel completeItem).
 struct FrameVar {
   float4* col;
-  int* queue;
-  const int* tileOrder;
-  int* tileCost;
-  int* tileCostMax;
-  int2* primHit;
   uint32_t sampleIndex;
-  uint32_t epoch;  // generation of everything else (scene, env, camera, tree, packets, bins)
+  uint32_t frameCounter;  // the frame's running-mean weight is 1/(frameCounter+1)
 };
 
 struct RenderParams {
@@ -225,13 +217,16 @@ struct RenderParams {
   int* tileCost;        // per tile: summed cost of its items this frame (shader cycles), null = not recorded
   int* tileCostMax;     // per tile: its longest item this frame
   unsigned long long* waveTrace;  // PT_WAVE_TRACE builds only: 6 u64 per wave (pt_runtime.cpp, tools/wave_trace.py)
-  // work sharing between frames in flight (FrameVar): null = this frame takes no other frame's items
-  FrameVar* frameVars;   // per slot
-  unsigned* frameReady;  // per slot: sequence number of the frame whose FrameVar is published there
-  uint32_t seq;          // this frame's sequence number
-  int depth;             // slots (frames in flight)
-  int shareAhead;        // most frames ahead of its own whose items a wave takes
-  uint32_t epoch;        // FrameVar::epoch of this frame
+  // frames in flight: this frame's sequence number, the slots, every slot's FrameVar
+  uint32_t seq;
+  int depth;
+  FrameVar* frameVars;
+  // The running mean updated inside the frame kernels (renderKernel completeItem), tile by tile in
+  // frame order: tileDone[(seq % (depth + 1)) * numItems + tile] counts the tile's pixels whose
+  // sample colour frame seq has written; mixState[tile] = 2 * (the next frame to mix into the
+  // tile) + 1 while a wave mixes it. null = mixKernel updates the running mean per frame.
+  int* tileDone;
+  unsigned* mixState;
 };
 
 struct TraceParams {
@@ -354,7 +349,7 @@ hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed,
 // the running-mean update of a pipelined frame over the rank's owned pixels (PackParams
 // mapping): accum = mix(accum, col, 1 / (frameCounter + 1)) (IS:868-871, pass2.fsh:15)
 hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s);
-// publish a frame's FrameVar in its slot (dst), then ready = seq (RenderParams::frameVars)
-hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, unsigned* ready, uint32_t seq, hipStream_t s);
+// publish a frame's FrameVar in its slot (dst) and zero the slot's work-queue counters
+hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, int* queue, hipStream_t s);
 
 }  // namespace pt

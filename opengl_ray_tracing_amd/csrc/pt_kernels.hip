@@ -286,8 +286,9 @@ __device__ __forceinline__ V3 cameraRay(const RenderParams& p, uint32_t sampleIn
 __device__ __forceinline__ void accumulate(const RenderParams& p, const FrameVar& f, int px, int py, V3 color, Counters& C,
                                            bool count) {
   float4* col = f.col;
-  if (!count && col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in order
-    stStream(col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
+  if (!count && col) {  // pipelined frame: the sample colour, mixed into the running mean in frame order
+    // (by another CU's wave, maybe in this launch: a write-through store, completeItem)
+    stCoherent(col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
     return;
   }
   float4* a = p.accum + (size_t)py * p.width + px;
@@ -857,6 +858,86 @@ __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
   return v;
 }
 
+// ------------------------------------------------ running mean inside the frame kernel
+// (RenderParams::tileDone / mixState; pt_runtime.cpp "frames in flight")
+__device__ __forceinline__ void tileOrigin(const RenderParams& p, int w, int& px0, int& py0) {
+  const int sub = p.shardSize >> 3;
+  const int j = w / p.shardTiles, s = w - j * p.shardTiles;
+  const int g = j * p.world + p.rank;
+  const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
+  px0 = gx * p.shardSize + (s % sub) * 8;
+  py0 = gy * p.shardSize + (s / sub) * 8;
+}
+// Frame `seq`'s item of tile w has written the sample colours of its pixels (valid lanes).
+// When that completes the tile for the frame, the wave brings the tile's running mean
+// (IS:868-871) up to date in frame order: it mixes the frame in if every earlier frame is
+// already mixed into the tile -- else the wave that mixes the frame before it will -- and
+// then each later frame that has already completed the tile. A per-tile lock word
+// (mixState = 2 * next frame to mix, + 1 while locked) admits one wave at a time and only for
+// the next frame in order. The completer counts, then tries the lock; the mixer unlocks,
+// then reads the next frame's count; each waits for its first access to complete before the
+// second, so a frame that completes the tile while another wave holds the lock is seen by
+// one of the two. Colours and the mean cross CUs as write-through (sc1) stores drained before
+// the count or the unlock and sc1 loads after it (stCoherent / ldCoherent): no cache
+// maintenance, and no wave ever waits for another. The image is the one of frames mixed
+// one after another (the same mixf, the same order).
+__device__ __forceinline__ void completeItem(const RenderParams& p, const FrameVar& fv, uint32_t seq, int w,
+                                             bool valid) {
+  const int lane = __lane_id();
+  const uint32_t D1 = (uint32_t)p.depth + 1u;
+  const int n = __popcll(__ballot(valid));
+  int px0, py0;
+  tileOrigin(p, w, px0, py0);
+  const int need = (px0 < p.width && py0 < p.height) ? min(8, p.width - px0) * min(8, p.height - py0) : 0;
+  if (need == 0) return;  // a tile of a shard wholly outside the image: no pixels, nothing to mix
+  drainStores();          // the wave's colour stores, before its count
+  int done = 0;
+  if (lane == 0)
+    done = __hip_atomic_fetch_add(p.tileDone + (size_t)(seq % D1) * p.numItems + w, n, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) + n;
+  if (__shfl(done, 0, 64) != need) return;
+  const int px = px0 + (lane & 7), py = py0 + (lane >> 3);
+  const bool in = px < p.width && py < p.height;
+  const size_t i = (size_t)py * p.width + px;
+  uint32_t g = seq;
+  // at most the frames in flight after seq can have completed the tile (bounded, come what may)
+  for (uint32_t k = 0; k <= (uint32_t)p.depth; k++) {
+    unsigned old = 2u * g;
+    if (lane == 0)
+      __hip_atomic_compare_exchange_strong(p.mixState + w, &old, 2u * g + 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)__shfl((int)old, 0, 64) != 2u * g) return;  // not g's turn yet, or locked: that wave mixes g
+    const float4* col = fv.col;
+    uint32_t fc = fv.frameCounter;
+    if (g != seq) {  // a later frame that completed the tile first: its published FrameVar
+      const FrameVar* v = p.frameVars + g % (uint32_t)p.depth;
+      const unsigned long long cb =
+          __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&v->col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      col = (const float4*)((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cb) |
+                            (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(cb >> 32)) << 32);
+      fc = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)__hip_atomic_load(&v->frameCounter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    if (in) {  // mixKernel's update of one pixel
+      const float4 c = ldCoherent(col + i);
+      const float4 a = ldCoherent(p.accum + i);
+      const float wt = 1.0f / (float)(fc + 1u);
+      stCoherent(p.accum + i, make_float4(mixf(a.x, c.x, wt), mixf(a.y, c.y, wt), mixf(a.z, c.z, wt), 1.0f));
+    }
+    drainStores();  // the tile's new mean, before the unlock
+    int next = 0;
+    if (lane == 0) {
+      __hip_atomic_store(p.tileDone + (size_t)(g % D1) * p.numItems + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.mixState + w, 2u * (g + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      drainStores();  // the unlock, before the next frame's count is read
+      next = __hip_atomic_load(p.tileDone + (size_t)((g + 1u) % D1) * p.numItems + w, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (__shfl(next, 0, 64) != need) return;  // the next frame has not completed the tile: its completer mixes it
+    g++;
+  }
+}
+
 // WAVES > 0: compiled for that many waves per SIMD (the latency-bound large
 // scenes' variant, pt_runtime.cpp renderFrame)
 template <int INTEG, bool CULL, bool COUNT, int WAVES = 0>
@@ -901,22 +982,13 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   // 0.59 -- the coherence of one tile's rays is worth more than full lanes.)
   const int waveId = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6), numWaves = gridDim.x * (BLOCK / 64);
   int dealt = 0;  // statically dealt items taken (band order)
-  // fv: the frame whose items this wave takes -- this launch's own frame, then (work
-  // sharing, RenderParams::frameVars) the next frames in flight. Kept in the wave's LDS
-  // slot and read where used, so none of it is live in registers across a path.
-  __shared__ FrameVar s_fv[BLOCK / 64];
-  FrameVar& fv = s_fv[threadIdx.x >> 6];
-  fv.col = p.col;  // every lane stores the same values (a wave's LDS accesses are in order)
-  fv.queue = p.queue;
-  fv.tileOrder = p.tileOrder;
-  fv.tileCost = p.tileCost;
-  fv.tileCostMax = p.tileCostMax;
-  fv.primHit = p.primHit;
+  // this launch's frame: its sample index, colour buffer and weight (completeItem, accumulate)
+  FrameVar fv;
+  fv.col = p.col;
   fv.sampleIndex = p.sampleIndex;
-  int ahead = 0;         // frames ahead of this launch's own frame
-  uint32_t shared = 0;   // items this wave took from later frames (pt_frame_stats.shared_items)
+  fv.frameCounter = p.frameCounter;
   auto claim = [&]() -> int {
-    if (p.staticItems > 0) {  // (frames dealing items statically share no work)
+    if (p.staticItems > 0) {
       const int t = waveId + dealt * numWaves;
       if (t < p.staticItems) {
         dealt++;
@@ -925,44 +997,12 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
       const int it = cur.next(p.queue, p.dynPerQueue, p.numItems - p.staticItems, home);
       return it < 0 ? it : p.staticItems + it;
     }
-    return cur.next(fv.queue, p.perQueue, p.numItems, home, fv.tileOrder, p.orderCap);
-  };
-  // the next frame in flight whose FrameVar is published (same epoch): its items are taken next
-  auto nextFrame = [&]() -> bool {
-    if (COUNT || !p.frameVars || ++ahead > p.shareAhead) return false;
-    const uint32_t want = p.seq + (uint32_t)ahead;
-    const int slot = (int)(want % (uint32_t)p.depth);
-    if (__hip_atomic_load(p.frameReady + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) return false;
-    const FrameVar* v = p.frameVars + slot;
-    // wave-uniform values: kept in scalar registers
-    auto ld32 = [](const uint32_t* a) {
-      return (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    };
-    auto ld64 = [&](void* const* a) {
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(a);
-      return (void*)((unsigned long long)ld32(w) | (unsigned long long)ld32(w + 1) << 32);
-    };
-    if (ld32(&v->epoch) != p.epoch) return false;
-    fv.col = (float4*)ld64((void* const*)&v->col);
-    fv.queue = (int*)ld64((void* const*)&v->queue);
-    fv.tileOrder = (const int*)ld64((void* const*)&v->tileOrder);
-    fv.tileCost = (int*)ld64((void* const*)&v->tileCost);
-    fv.tileCostMax = (int*)ld64((void* const*)&v->tileCostMax);
-    fv.primHit = (int2*)ld64((void* const*)&v->primHit);
-    fv.sampleIndex = ld32(&v->sampleIndex);
-    cur = TileCursor();
-    return true;
+    return cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
   };
   int item = claim();
-  while (true) {
-    if (item < 0) {
-      if (!nextFrame()) break;
-      item = claim();
-      continue;
-    }
-    if (!COUNT && ahead > 0) shared++;
+  while (item >= 0) {
 #if PT_CLAIM_AHEAD
-    cur.claimAhead(fv.queue, home);
+    cur.claimAhead(p.queue, home);
 #endif
     const int w = itemTile(item);
     const long long t0 = COUNT ? 0 : clock64();
@@ -979,15 +1019,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     const int px = gx * p.shardSize + (s % sub) * 8 + (k & 7);
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
     const bool valid = lane < nLanes && px < p.width && py < p.height;
-    int2* const primHit = fv.primHit;
-    if (!COUNT && primHit) {  // camera rays already traced by primaryKernel
-      int2 h = make_int2(PRIM_MISS, 0);
-      if (valid) {  // through L2: another frame in flight's results may be read here (work sharing)
-        const unsigned long long b = __hip_atomic_load(
-            reinterpret_cast<const unsigned long long*>(primHit + (size_t)py * p.width + px), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        h = make_int2((int)(uint32_t)b, (int)(uint32_t)(b >> 32));
-      }
+    if (!COUNT && p.primHit) {  // camera rays already traced by primaryKernel
+      const int2 h = valid ? p.primHit[(size_t)py * p.width + px] : make_int2(PRIM_MISS, 0);
       int tri = h.x;
       float t = __int_as_float(h.y);
       if (__ballot(valid && tri == PRIM_TILE)) {  // wave-uniform: the whole tile
@@ -1009,10 +1042,11 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
       const int tri = primaryPixel<CULL, COUNT>(p, fv, px, py, st, C, top, t);
       if (tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, fv, px, py, tri, t, st, C, top);
     }
-    if (!COUNT && lane == 0 && fv.tileCost) {
+    if (!COUNT && p.mixState) completeItem(p, fv, p.seq, w, valid);
+    if (!COUNT && p.tileCost && lane == 0) {
       const int dt = (int)min(clock64() - t0, (long long)0x3fffffff);
-      atomicAdd(fv.tileCost + w, dt);
-      atomicMax(fv.tileCostMax + w, dt);
+      atomicAdd(p.tileCost + w, dt);
+      atomicMax(p.tileCostMax + w, dt);
     }
 #if PT_WAVE_TRACE
     const unsigned long long tEnd = wall_clock64();
@@ -1031,7 +1065,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     }
 #endif
 #if PT_CLAIM_AHEAD
-    item = cur.nextAhead(fv.queue, p.perQueue, p.numItems, home, fv.tileOrder, p.orderCap);
+    item = cur.nextAhead(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
 #else
     item = claim();
 #endif
@@ -1044,8 +1078,6 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   }
 #endif
   addRays(p.rayShards, C.rays);
-  if (!COUNT && shared && lane == 0)
-    atomicAdd(reinterpret_cast<unsigned long long*>(p.stats + 5), (unsigned long long)shared);
   if (COUNT) {
     uint32_t n = waveSum(C.nodes), t = waveSum(C.tris), m = waveSum(C.mats), x = waveSum(C.texels);
     if (lane == 0) {
@@ -1240,12 +1272,19 @@ hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint
   hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + bs - 1) / bs)), dim3(bs), 0, s, p, accum, col, frameCounter);
   return hipGetLastError();
 }
-__global__ void frameVarKernel(FrameVar v, FrameVar* dst, unsigned* ready, uint32_t seq) {
-  *dst = v;
-  __hip_atomic_store(ready, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // after the FrameVar
+// A frame's FrameVar published in its slot (read by earlier frames' waves during their
+// launches: write-through 8-byte stores), and the slot's work-queue counters zeroed: one
+// 64-thread launch instead of a FrameVar copy and a memset
+__global__ void frameVarKernel(FrameVar v, FrameVar* dst, int* queue) {
+  static_assert(sizeof(FrameVar) % 8 == 0, "FrameVar in 8-byte words");
+  const int t = threadIdx.x;
+  if (t < (int)(sizeof(FrameVar) / 8))
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + t, reinterpret_cast<const unsigned long long*>(&v)[t],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t < NUM_QUEUES) queue[t * CTL_LINE_INTS] = 0;
 }
-hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, unsigned* ready, uint32_t seq, hipStream_t s) {
-  hipLaunchKernelGGL(frameVarKernel, dim3(1), dim3(1), 0, s, v, dst, ready, seq);
+hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, int* queue, hipStream_t s) {
+  hipLaunchKernelGGL(frameVarKernel, dim3(1), dim3(64), 0, s, v, dst, queue);
   return hipGetLastError();
 }
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s) {

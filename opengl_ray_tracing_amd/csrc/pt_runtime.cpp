@@ -141,15 +141,18 @@ struct pt_ctx {
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
   bool gridShare = true;                    // frames in flight split the persistent grid (PT_GRID_SHARE=0: not)
   int gridPct = 100;                        // % of residency the frames in flight split (PT_GRID_PCT)
-  // work sharing between frames in flight (renderKernel, FrameVar; PT_SHARE_WORK=1: on)
-  bool shareWork = false;
-  // frames ahead of its own whose items a wave may take (PT_SHARE_AHEAD): a kernel lasts until
-  // the last of them is claimed out, and its slot's next frame cannot start before it ends
-  int shareAhead = 1;
-  FrameVar* d_frameVars = nullptr;          // per slot
-  unsigned* d_frameReady = nullptr;         // per slot: sequence number of the published frame
-  uint32_t shareEpoch = 0;                  // FrameVar::epoch: bumped when anything else a frame reads changes
-  unsigned long long shareKey[3] = {~0ull, ~0ull, ~0ull};  // what the epoch was issued for (renderOne)
+  // the running mean updated tile by tile inside the frame kernels (renderKernel completeItem;
+  // PT_KERNEL_MIX=1; off: mixKernel per frame on the caller's stream): per colour buffer and tile
+  // the pixels written, per tile the lock word (2 x next frame to mix); valid from frame
+  // protoNext on while protoValid, re-initialised (after every earlier frame) otherwise
+  bool kernelMix = false;
+  int* d_tileDone = nullptr;
+  unsigned* d_mixState = nullptr;
+  bool protoValid = false;
+  unsigned long long protoNext = 0;
+  hipEvent_t protoInit = nullptr, callerMark = nullptr;
+  unsigned protoGen = 0, protoGenSeen[MAX_SLOTS] = {};
+  FrameVar* d_frameVars = nullptr;          // per slot: the published FrameVar (frameVarKernel)
   hipStream_t slotStream[PIPE] = {};
   hipEvent_t kernelDone[PIPE] = {};         // slot's last frame kernel (+ reorder) ended
   bool slotBusy[PIPE] = {};                 // kernelDone[k] has been recorded since the last sync
@@ -343,13 +346,10 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     if (const char* e = std::getenv("PT_PIPE_DEPTH")) ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
-    if (const char* e = std::getenv("PT_SHARE_WORK")) ctx->shareWork = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PT_SHARE_AHEAD")) ctx->shareAhead = std::max(1, std::atoi(e));
-    // work sharing between frames in flight (renderKernel, FrameVar): per slot the published
-    // frame variables and the sequence number of the frame they belong to (none yet: ~0)
+    if (const char* e = std::getenv("PT_KERNEL_MIX")) ctx->kernelMix = std::atoi(e) != 0;
+    CKC(hipEventCreateWithFlags(&ctx->protoInit, hipEventDisableTiming));
+    CKC(hipEventCreateWithFlags(&ctx->callerMark, hipEventDisableTiming));
     CKC(hipMalloc(&ctx->d_frameVars, PIPE * sizeof(FrameVar)));
-    CKC(hipMalloc(&ctx->d_frameReady, PIPE * sizeof(unsigned)));
-    CKC(hipMemset(ctx->d_frameReady, 0xff, PIPE * sizeof(unsigned)));
     // slot streams are created as a depth first uses them (ensureSlots): streams beyond the
     // hardware queues share queues, which serialises their work
     for (int k = 0; k < COLS; k++) CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
@@ -418,7 +418,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
-  dfree(ctx->d_frameVars); dfree(ctx->d_frameReady);
+  dfree(ctx->d_frameVars); dfree(ctx->d_tileDone); dfree(ctx->d_mixState);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
   freePrimaryBins(ctx->bins);
   for (int k = 0; k < PIPE; k++) {
@@ -1654,7 +1654,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // results reset for this frame
   if (piped && ctx->frameNo >= (unsigned long long)(D + 1)) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
   int* queue = reinterpret_cast<int*>(ctx->d_ctl + CTL_QUEUES) + (size_t)slot * NUM_QUEUES * CTL_LINE_INTS;
-  CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
+  // (the in-kernel running mean's frames zero them in frameVarKernel, right before the frame kernel)
+  if (!(piped && D > 1 && ctx->kernelMix && !regen))
+    CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   RenderParams p;
   std::memset(&p, 0, sizeof(p));
   p.scene = sceneView(ctx);
@@ -1775,33 +1777,42 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (piped && probing) {
     if (int e = waitOthers()) return e;
   }
-  // Work sharing between frames in flight (renderKernel, FrameVar): this frame publishes its
-  // FrameVar so that waves of earlier frames in flight whose own items are exhausted take its
-  // items; and its waves take later frames' items. Not while the policy probe times frames,
-  // nor with statically dealt items. The epoch changes whenever anything else the frame
-  // reads (camera, scene, env, tree, packets, bins) differs from the previous frame's.
-  const bool share = piped && D > 1 && ctx->shareWork && !regen && !probing && p.staticItems == 0;
-  if (share) {
-    unsigned long long h = 1469598103934665603ull;  // FNV-1a of the camera
-    auto mixIn = [&](const void* b, size_t n) {
-      for (size_t i = 0; i < n; i++) h = (h ^ reinterpret_cast<const unsigned char*>(b)[i]) * 1099511628211ull;
-    };
-    mixIn(eye, 3 * sizeof(float));
-    mixIn(cameraRotate, 16 * sizeof(float));
-    const unsigned long long key[3] = {
-        h, (unsigned long long)(p.scene.fast | p.packets << 1 | (p.binStart ? 4 : 0) | (p.primHit ? 8 : 0)) |
-               (unsigned long long)ctx->sceneVersion << 8 | (unsigned long long)ctx->policyKey << 36,
-        (unsigned long long)ctx->binGen};
-    if (std::memcmp(key, ctx->shareKey, sizeof(key))) {
-      ctx->shareEpoch++;
-      std::memcpy(ctx->shareKey, key, sizeof(key));
+  // The running mean inside the frame kernels (completeItem): every pipelined megakernel
+  // frame, once the tile protocol's state is valid for it -- else, first, after every
+  // earlier frame and the caller's stream's work so far (a cleared accumulation), the
+  // state is reset on this frame's stream and every slot's next frame waits for that.
+  const bool proto = piped && D > 1 && ctx->kernelMix && !regen;
+  if (proto) {
+    if (!ctx->d_tileDone) {
+      CK(hipMalloc(&ctx->d_tileDone, (size_t)COLS * ctx->numItems * sizeof(int)));
+      CK(hipMalloc(&ctx->d_mixState, (size_t)ctx->numItems * sizeof(unsigned)));
     }
+    if (!ctx->protoValid || ctx->protoNext != ctx->frameNo) {
+      CK(hipEventRecord(ctx->callerMark, ctx->stream));
+      CK(hipStreamWaitEvent(S, ctx->callerMark, 0));
+      for (int k = 0; k < D; k++)
+        if (k != slot && ctx->slotBusy[k]) CK(hipStreamWaitEvent(S, ctx->kernelDone[k], 0));
+      if (ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastCol], 0));
+      CK(hipMemsetAsync(ctx->d_tileDone, 0, (size_t)COLS * ctx->numItems * sizeof(int), S));
+      CK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->d_mixState), (int)(2u * (uint32_t)ctx->frameNo),
+                           (size_t)ctx->numItems, S));
+      CK(hipEventRecord(ctx->protoInit, S));
+      ctx->protoGen++;
+      ctx->protoGenSeen[slot] = ctx->protoGen;
+      ctx->protoValid = true;
+    }
+    if (ctx->protoGenSeen[slot] != ctx->protoGen) {
+      CK(hipStreamWaitEvent(S, ctx->protoInit, 0));
+      ctx->protoGenSeen[slot] = ctx->protoGen;
+    }
+    ctx->protoNext = ctx->frameNo + 1;
+    p.tileDone = ctx->d_tileDone;
+    p.mixState = ctx->d_mixState;
     p.frameVars = ctx->d_frameVars;
-    p.frameReady = ctx->d_frameReady;
     p.seq = (uint32_t)ctx->frameNo;
     p.depth = D;
-    p.shareAhead = std::min(ctx->shareAhead, D - 1);
-    p.epoch = ctx->shareEpoch;
+  } else if (piped) {
+    ctx->protoValid = false;  // this frame's running mean is mixKernel's
   }
   int erc = launchEvents(ctx, &evb, &eve);
   if (erc) return erc;
@@ -1819,28 +1830,15 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
 #endif
   CK(hipEventRecord(evb, S));
   if (p.primHit) CK(launchPrimary(p, S));
-  if (share) {
+  if (proto) {  // its FrameVar for the earlier frames' waves that may mix its tiles; its queue counters zeroed
     FrameVar fv;
     fv.col = p.col;
-    fv.queue = p.queue;
-    fv.tileOrder = p.tileOrder;
-    fv.tileCost = p.tileCost;
-    fv.tileCostMax = p.tileCostMax;
-    fv.primHit = p.primHit;
     fv.sampleIndex = p.sampleIndex;
-    fv.epoch = p.epoch;
-    CK(launchFrameVar(fv, ctx->d_frameVars + slot, ctx->d_frameReady + slot, p.seq, S));
+    fv.frameCounter = p.frameCounter;
+    CK(launchFrameVar(fv, ctx->d_frameVars + slot, queue, S));
   }
   if (regen) CK(launchRegen(p, c.integrator, grid, S, cull, wide));
   else CK(launchRender(p, c.integrator, grid, S, cull, count, wide));
-  // With work sharing, waves of earlier frames may still be taking this frame's items after
-  // its own kernel has ended: the frame counts as ended (kernelDone, and before that the
-  // reorder that rewrites this slot's order list) once the previous frame has ended too, so
-  // by induction once every earlier frame has.
-  if (share && ctx->frameNo >= 1) {
-    const int prev = (int)((ctx->frameNo - 1) % (unsigned)D);
-    if (ctx->slotBusy[prev]) CK(hipStreamWaitEvent(S, ctx->kernelDone[prev], 0));
-  }
 #if PT_WAVE_TRACE
   if (dTrace) {
     std::vector<unsigned long long> tr(nTrace);
@@ -1863,7 +1861,26 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // kernel_ms: the frame's own kernels (camera-ray pass, frame kernel, reorder), so the
   // policy probe weighs the order's cost too; the running-mean update below is not in it
   CK(hipEventRecord(eve, S));
-  if (piped) {
+  if (proto) {
+    // A tile's mix of frame g runs in a kernel up to g's own, so the frame is mixed in once
+    // every kernel up to its own has ended: its end waits for the previous frame's end (by
+    // induction, every earlier frame's). The caller's stream follows it (whatever the caller
+    // queues behind the frame sees its update).
+    if (ctx->frameNo >= 1) {
+      const int prev = (int)((ctx->frameNo - 1) % (unsigned)D);
+      if (ctx->slotBusy[prev]) CK(hipStreamWaitEvent(S, ctx->kernelDone[prev], 0));
+    }
+    // follows it (whatever the caller queues behind the frame sees its update)
+    CK(hipEventRecord(ctx->kernelDone[slot], S));
+    ctx->slotBusy[slot] = true;
+    CK(hipEventRecord(ctx->mixDone[colIdx], S));
+    CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[colIdx], 0));
+    ctx->lastMixStream = ctx->stream;
+    ctx->lastSlot = slot;
+    ctx->lastCol = colIdx;
+    ctx->mixPending = true;
+    ctx->frameNo++;
+  } else if (piped) {
     // the running-mean update on the caller's stream, in frame order, after this frame's kernel
     CK(hipEventRecord(ctx->kernelDone[slot], S));
     ctx->slotBusy[slot] = true;
@@ -2002,6 +2019,7 @@ int pt_clear_accum(pt_ctx* ctx) {
   if (int rc = joinGather(ctx)) return rc;
   for (pt_ctx* m : members(ctx)) {
     if (int rc = joinPipe(m)) return fromPeer(ctx, m, rc);
+    m->protoValid = false;  // the next frame's kernel updates the accumulation after this clear
     if (hipSetDevice(m->cfg.device_id) != hipSuccess ||
         hipMemsetAsync(m->d_accum, 0, (size_t)m->cfg.width * m->cfg.height * sizeof(float4), m->stream) != hipSuccess)
       return fail(ctx, PT_E_HIP, "pt_clear_accum on device " + std::to_string(m->cfg.device_id));
@@ -2129,7 +2147,6 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
     st->kernel_ms_total = std::max(st->kernel_ms_total, q.kernel_ms_total);
     st->max_stack = std::max(st->max_stack, q.max_stack);
     st->split_items += q.split_items;
-    st->shared_items += q.shared_items;
   }
   st->devices = 1 + (int)ctx->peers.size();
   st->gather = ctx->gather ? ctx->gather->mode : 0;
@@ -2138,7 +2155,7 @@ int pt_get_stats(pt_ctx* ctx, pt_frame_stats* st) {
 
 static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   if (int rc = syncStreams(ctx)) return rc;
-  unsigned long long h[6];
+  unsigned long long h[5];
   std::vector<unsigned long long> shards((size_t)RAY_SHARDS * RAY_SHARD_STRIDE);
   CK(hipMemcpy(h, ctx->d_ctl + CTL_STATS, sizeof(h), hipMemcpyDeviceToHost));
   CK(hipMemcpy(shards.data(), ctx->d_ctl + CTL_RAYS, shards.size() * sizeof(unsigned long long),
@@ -2150,7 +2167,6 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->tri_fetch = h[2];
   st->mat_fetch = h[3];
   st->tex_fetch = h[4];
-  st->shared_items = (int)h[5];
   while (foldOne(ctx, true)) {
   }
   st->kernel_ms = ctx->launches > 0 ? ctx->msLast : 0.0f;

@@ -791,11 +791,6 @@ constexpr int MAX_SPLIT_LG = PT_MAX_SPLIT_LG;
 __device__ __forceinline__ int itemTile(int item) { return item & ((1 << ITEM_TILE_BITS) - 1); }
 __device__ __forceinline__ int itemSub(int item) { return (item >> ITEM_TILE_BITS) & 63; }
 __device__ __forceinline__ int itemLg(int item) { return (item >> 28) & 7; }
-// a load that reads L2 (never a stale per-CU cache line): data another frame in flight
-// published during this kernel (FrameVar's order lists and camera-ray results)
-__device__ __forceinline__ int ldShared(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 struct TileCursor {
   int qi = 0;  // queues found empty (wave-uniform)
   __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home, const int* order = nullptr,
@@ -805,8 +800,8 @@ struct TileCursor {
       int it = 0;
       if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
       it = __shfl(it, 0, 64);
-      if (order) {  // the list may belong to another frame in flight (work sharing): read through L2
-        if (it < ldShared(order + NUM_QUEUES * orderCap + q)) return ldShared(order + q * orderCap + it);
+      if (order) {
+        if (it < order[NUM_QUEUES * orderCap + q]) return order[q * orderCap + it];
       } else {
         const int t = q * perQueue + it;
         if (it < perQueue && t < numItems) return t;

@@ -63,7 +63,6 @@ class FrameStats:
     accel_nodes: int = 0
     accel_depth: int = 0
     regen: int = 0
-    shared_items: int = 0  # work items of a frame in flight taken by an earlier frame's waves
 
 
 def _fp(a: np.ndarray):
@@ -267,8 +266,7 @@ class Renderer:
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
                           s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
                           s.waves_per_simd, s.devices, s.gather, s.frames_in_flight, s.upload_ms,
-                          s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth, s.regen,
-                          s.shared_items)
+                          s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth, s.regen)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")
