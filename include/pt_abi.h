@@ -60,8 +60,9 @@ extern "C" {
                                        the frame kernel instead of inside it: same images; the default for
                                        the large-scene regen kernel (c5 -9 %), slower for the megakernel
                                        on c2-c4. PT_FLAG_NO_BINS turns the pass off */
-#define PT_FLAG_MEGAKERNEL 0x400u /* large scenes (> 48 MB of records): the lock-step megakernel instead of
-                                     the path-regeneration kernel the Disney/MIS integrators default to there */
+#define PT_FLAG_MEGAKERNEL 0x400u /* the lock-step megakernel instead of the path-regeneration kernel (4-wide
+                                     walk with dynamic ray fetch, camera-ray pass) that large scenes (> 48 MB
+                                     of records) and the Lambert integrator on any scene default to */
 #define PT_FLAG_HOST_ACCEL 0x200u /* pt_upload_scene builds the runtime's own tree on the host (threaded binned
                                      SAH) instead of on the GPU (pt_build.hip) */
 

@@ -350,12 +350,12 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
 
 template <int I>
 static const void* regenFn(bool cull, bool wide) {
-  if (wide && I != 0) return (const void*)regenKernel<I, true, WIDE_REGEN_WAVES, true>;
+  if (wide) return (const void*)regenKernel<I, true, WIDE_REGEN_WAVES, true>;
   return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
 }
 template <int I>
 static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, bool wide) {
-  if (wide && cull && I != 0)
+  if (wide && cull)
     hipLaunchKernelGGL((regenKernel<I, true, WIDE_REGEN_WAVES, true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else hipLaunchKernelGGL((regenKernel<I, false>), dim3(grid), dim3(BLOCK), 0, s, p);

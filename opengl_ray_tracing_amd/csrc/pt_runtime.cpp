@@ -146,6 +146,11 @@ struct pt_ctx {
   // the pixels written, per tile the lock word (2 x next frame to mix); valid from frame
   // protoNext on while protoValid, re-initialised (after every earlier frame) otherwise
   bool kernelMix = false;
+  // the large-scene path (regen kernel at 4 waves/SIMD, 4-wide walk with dynamic ray fetch,
+  // camera-ray pass) on scenes of any size: -1 = for the Lambert integrator (c2 0.342 ->
+  // 0.251 ms/frame; MIS c4 0.355 -> 0.468, Disney-MIS c3 0.160 -> 0.163: those keep the
+  // megakernel), 1 = every integrator, 0 = large scenes only (PT_REGEN_WIDE)
+  int regenWide = -1;
   int* d_tileDone = nullptr;
   unsigned* d_mixState = nullptr;
   bool protoValid = false;
@@ -334,6 +339,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   ctx->perQueue = (ctx->numItems + NUM_QUEUES - 1) / NUM_QUEUES;
   // the default megakernel pipelines its frames (not BASIC, the fetch counter, the
   // wavefront / regeneration kernels or PT_FLAG_SERIAL_FRAMES)
+  if (const char* e = std::getenv("PT_REGEN_WIDE")) ctx->regenWide = std::atoi(e) != 0 ? 1 : 0;
   ctx->pipe = cfg->integrator != PT_BASIC_CPU_COMPAT &&
               !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_WAVEFRONT | PT_FLAG_REGEN | PT_FLAG_SERIAL_FRAMES));
   if (ctx->pipe) {
@@ -1602,7 +1608,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // leave a lock-step wave's lanes idle
   const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + HIT_F4 * 16) + (size_t)ctx->nDevNodes * 64;
   const bool wideScene = !count && cull && c.integrator != 0 && sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
-  const bool regen = !count && ((c.flags & PT_FLAG_REGEN) || (wideScene && !(c.flags & PT_FLAG_MEGAKERNEL)));
+  const bool regenAll = !count && cull && (ctx->regenWide > 0 || (ctx->regenWide < 0 && c.integrator == 0));
+  const bool regen =
+      !count && ((c.flags & PT_FLAG_REGEN) || ((wideScene || regenAll) && !(c.flags & PT_FLAG_MEGAKERNEL)));
   // this frame's stream and per-frame buffers: slot frameNo % depth, colour buffer
   // frameNo % (depth + 1) when pipelined
   const bool piped = ctx->pipe && !count;
@@ -1621,7 +1629,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     return PT_OK;
   };
   int nb = 0;
-  const bool wide = wideScene;  // the more-waves variant of either kernel
+  // the more-waves variant of either kernel (PT_REGEN_WIDE=1: the regen kernel's on any scene,
+  // with its 4-wide walk, dynamic ray fetch and camera-ray pass)
+  const bool wide = wideScene || (regen && regenAll);
   if (regen) CK(regenBlocksPerCU(c.integrator, cull, wide, &nb));
   else CK(renderBlocksPerCU(c.integrator, cull, count, wide, &nb));
   if (nb < 1) nb = 1;

@@ -387,15 +387,16 @@ def test_camera_restart_keeps_policies_and_restarts_the_mean(name):
 def test_band_order_frames_equal_ordered_frames(name):
     """Frames handed out in band order (PT_FLAG_NO_TILE_ORDER, and the probe's band-order trial
     frames 15-16 of pt_runtime.cpp probePolicy) give the longest-first frames' image bit for bit,
-    across the probe and a camera restart."""
-    from opengl_ray_tracing_amd import FLAG_NO_TILE_ORDER
+    across the probe and a camera restart (the megakernel's tile hand-out: FLAG_MEGAKERNEL, as
+    Lambert frames default to the regen kernel)."""
+    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_NO_TILE_ORDER
     cfg, tris, nodes, hdr = scenes.build_config(name)
     w, h = 480, 270
     a = orbit_camera(*cfg.camera)
     b = orbit_camera(cfg.camera[0] + 7.0, cfg.camera[1] + 3.0, cfg.camera[2])
 
     def run(flags):
-        with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=flags) as r:
+        with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=flags | FLAG_MEGAKERNEL) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
             for f in range(24):

@@ -144,22 +144,27 @@ def test_fetch_counts_match_oracle(c2):
 
 @pytest.mark.parametrize("name,integrator", [("c2", "lambert"), ("c3", "disney"), ("c3", "mis"), ("c4", "mis")])
 def test_frame_kernels_agree(request, name, integrator):
-    """The lock-step megakernel (default), the path-regeneration kernel (FLAG_REGEN) and the
-    wavefront pipeline (FLAG_WAVEFRONT) give bit-identical images."""
-    from opengl_ray_tracing_amd import FLAG_REGEN, FLAG_WAVEFRONT
+    """The lock-step megakernel (FLAG_MEGAKERNEL; the default for Disney/MIS on small scenes),
+    the path-regeneration kernel (FLAG_REGEN), its large-scene form (the default for Lambert:
+    4-wide walk with dynamic ray fetch, camera-ray pass) and the wavefront pipeline
+    (FLAG_WAVEFRONT) give bit-identical images."""
+    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_REGEN, FLAG_WAVEFRONT
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     mb = {"disney": 5}.get(integrator, cfg.max_bounce)
     a, sa = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_REGEN)
-    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb)
+    b, sb = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_MEGAKERNEL)
     c, sc = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_WAVEFRONT)
+    d, sd = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb)
+    assert sb.regen == 0 and sd.regen == (1 if integrator == "lambert" else 0)
     assert np.array_equal(a, b)
     assert np.array_equal(c, b)
+    assert np.array_equal(d, b)
     if integrator == "mis":
         # regeneration and wavefront skip BRDF rays whose pdf is 0 (IS:816 discards them after tracing)
         assert sa.rays == sc.rays
         assert sb.rays >= sa.rays >= 0.95 * sb.rays
     else:
-        assert sa.rays == sb.rays == sc.rays
+        assert sa.rays == sb.rays == sc.rays == sd.rays
 
 
 @pytest.mark.parametrize("name,integrator", [("c2", "lambert"), ("c3", "disney"), ("c3", "mis"), ("c4", "mis")])
@@ -238,8 +243,8 @@ def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
     o, _ = render_oracle(cfg, tris, nodes, hdr, px, frames=2, max_bounce=mb, w=w, h=h)
     parity.assert_parity(g[px[:, 1], px[:, 0]], o[px[:, 1], px[:, 0]], "wide/mis")
     assert np.all(g[..., 3] == 1.0)
-    # the uniform Disney integrator (D:443-481) takes the same large-scene kernel; Lambert keeps
-    # the megakernel (its paths are short)
+    # the uniform Disney integrator (D:443-481) takes the same large-scene kernel, and so does
+    # Lambert (on every scene)
     d, sd = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator="disney", max_bounce=mb, w=w, h=h)
     dm, sdm = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator="disney", max_bounce=mb, w=w, h=h,
                          flags=FLAG_MEGAKERNEL)
@@ -248,20 +253,23 @@ def test_large_scene_runs_the_wide_kernel_and_matches_oracle():
     od, _ = render_oracle(cfg, tris, nodes, hdr, px, frames=2, integrator="disney", max_bounce=mb, w=w, h=h)
     parity.assert_parity(d[px[:, 1], px[:, 0]], od[px[:, 1], px[:, 0]], "wide/disney")
     _, sl = render_gpu(cfg, tris, nodes, hdr, frames=1, integrator="lambert", max_bounce=mb, w=w, h=h)
-    assert sl.regen == 0
+    assert sl.regen == 1
 
 
 @pytest.mark.parametrize("name,tile,depth", [("c4", (0, 1), None), ("c2", (1, 3), None), ("c4", (0, 1), 3),
-                                              ("c2", (1, 3), 8)])
+                                              ("c2", (1, 3), 8), ("c2m", (0, 1), None)])
 def test_pipelined_frames_equal_serial_frames(request, monkeypatch, name, tile, depth):
     """Frames in flight (the default: frame f+1's megakernel overlaps frame f's tail, each
     frame's running-mean update runs in frame order) give the image of serial frames
     (PT_FLAG_SERIAL_FRAMES) bit for bit -- through the policy probes (the depth probe drains
     and changes the pipeline depth mid-stream), a camera reset, images read mid-stream and a
     screen-tile shard, and at fixed depths 3 and 8 (PT_PIPE_DEPTH) -- with the same rays."""
-    from opengl_ray_tracing_amd import FLAG_SERIAL_FRAMES
+    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_SERIAL_FRAMES
     if depth is not None:
         monkeypatch.setenv("PT_PIPE_DEPTH", str(depth))
+    extra = 0
+    if name == "c2m":  # c2 through the megakernel (Lambert defaults to the regen kernel)
+        name, extra = "c2", FLAG_MEGAKERNEL
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     eye, rot = orbit_camera(*cfg.camera)
     eye2, rot2 = orbit_camera(30.0, 15.0, 4.0)
@@ -270,7 +278,7 @@ def test_pipelined_frames_equal_serial_frames(request, monkeypatch, name, tile, 
 
     def run(flags):
         out = []
-        with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=flags, tile_rank=tile[0],
+        with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=flags | extra, tile_rank=tile[0],
                       tile_world=tile[1]) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
@@ -302,10 +310,11 @@ def test_kernel_running_mean_equals_serial_frames(request, monkeypatch, name, ti
     from opengl_ray_tracing_amd import FLAG_PRIMARY_PASS, FLAG_SERIAL_FRAMES
     monkeypatch.setenv("PT_PIPE_DEPTH", "8")
     monkeypatch.setenv("PT_KERNEL_MIX", "1")  # opt-in (measured slower than mixKernel)
+    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     eye, rot = orbit_camera(*cfg.camera)
     w, h = 960, 540
-    extra = FLAG_PRIMARY_PASS if flags == "primary" else 0
+    extra = (FLAG_PRIMARY_PASS if flags == "primary" else 0) | FLAG_MEGAKERNEL  # the protocol is the megakernel's
 
     def run(fl):
         out = []
@@ -372,7 +381,7 @@ def test_camera_ray_pass_equals_megakernel_camera_rays(request, name, integrator
     megakernel / the path-regeneration kernel bit for bit: near and far cameras (the far one
     fills bins past PT_BIN_CAP, whose tiles the frame kernel traces itself), a camera move and
     a shard."""
-    from opengl_ray_tracing_amd import FLAG_PRIMARY_PASS, FLAG_REGEN
+    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_PRIMARY_PASS, FLAG_REGEN
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     cams = [orbit_camera(*cfg.camera), orbit_camera(40.0, 25.0, 1.5), orbit_camera(-70.0, -10.0, 14.0)]
     w, h = 960, 540
@@ -389,7 +398,7 @@ def test_camera_ray_pass_equals_megakernel_camera_rays(request, name, integrator
                 out.append(r.accum())
             return out, r.stats()
 
-    base = FLAG_REGEN if regen else 0
+    base = FLAG_REGEN if regen else FLAG_MEGAKERNEL
     a, sa = run(base)
     b, sb = run(base | FLAG_PRIMARY_PASS)
     for x, y in zip(a, b):
