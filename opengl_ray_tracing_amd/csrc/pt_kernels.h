@@ -338,6 +338,7 @@ hipError_t launchPrimary(const RenderParams& p, hipStream_t s);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool wide = false);
 hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb);
 int regenLdsStack();
+int regenTop4();  // 4-wide nodes the wide regen kernel stages in LDS (PT_REGEN_TOP4)
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s);

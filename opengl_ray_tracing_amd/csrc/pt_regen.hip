@@ -47,6 +47,14 @@ constexpr int REGEN_LDS_STACK = PT_REGEN_LDS_STACK;
 #define PT_REGEN_MIN_WAVES_MIS 1
 #endif
 
+// 4-wide nodes of the runtime tree (breadth-first ids) the wide variant stages in LDS per block:
+// 128 (16 KB, with the 16 KB stack rows 4 blocks per CU) measured c2 0.248 -> 0.245 ms and
+// c5 7.98 -> 7.28 ms against 64; 192 (the LDS limit at 4 blocks) c2 0.247, c5 7.60
+#ifndef PT_REGEN_TOP4
+#define PT_REGEN_TOP4 128
+#endif
+constexpr int REGEN_TOP4 = PT_REGEN_TOP4;
+
 enum : int { K_NONE = 0, K_PRIMARY = 1, K_BOUNCE = 2, K_SHADOW = 3 };
 
 struct PathState {
@@ -242,7 +250,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   st.reset();
   // the top of the uploaded tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
-  __shared__ float4 s_nodes[LDS_NODES * 4];
+  constexpr int TOPF4 = (W4 && REGEN_TOP4 * W4_F4 > LDS_NODES * 4) ? REGEN_TOP4 * W4_F4 : LDS_NODES * 4;
+  __shared__ float4 s_nodes[TOPF4];
   {
     const bool w4 = W4 && p.scene.fast;
     const float4* src = w4 ? p.scene.fbvh4 : p.scene.bvh;
@@ -268,6 +277,12 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   PathState s;
   s.px = s.py = 0;
   s.kind = K_NONE;
+#if PT_WAVE_TRACE
+  // diagnostics build: {start, end, tiles | last lone lane's pixel << 32, last successful claim,
+  // loop iterations, iterations with at most 4 lanes active} (100 MHz wall clock, tools/wave_trace.py --regen)
+  const unsigned long long wStart = wall_clock64();
+  unsigned long long wTiles = 0, wLastClaim = wStart, wIters = 0, wThin = 0, wLonePix = 0;
+#endif
   while (true) {
     // regenerate: idle lanes take the next pixels of the wave's tile
     while (true) {
@@ -278,6 +293,10 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
         if (item < 0) break;  // no tiles left for this wave
         tile = item;
         cursor = 0;
+#if PT_WAVE_TRACE
+        wTiles++;
+        wLastClaim = wall_clock64();
+#endif
       }
       const int slot = cursor + __popcll(idle & below);
       if (!active && slot < 64) {
@@ -307,7 +326,16 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
       }
       cursor = min(64, cursor + __popcll(idle));
     }
-    if (__ballot(active) == 0) break;
+    const unsigned long long act = __ballot(active);
+    if (act == 0) break;
+#if PT_WAVE_TRACE
+    wIters++;
+    if (__popcll(act) <= 4) {
+      wThin++;
+      const int l = __ffsll((long long)act) - 1;
+      wLonePix = (unsigned long long)__shfl(s.px, l, 64) << 16 | (unsigned long long)__shfl(s.py, l, 64);
+    }
+#endif
     if (!active) continue;
     float t;
     int tri;
@@ -345,6 +373,13 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
       active = false;
     }
   }
+#if PT_WAVE_TRACE
+  if (p.waveTrace && lane == 0) {
+    unsigned long long* r = p.waveTrace + 6 * ((size_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
+    r[0] = wStart; r[1] = wall_clock64(); r[2] = wTiles | wLonePix << 32; r[3] = wLastClaim;
+    r[4] = wIters; r[5] = wThin;
+  }
+#endif
   addRays(p.rayShards, C.rays);
 }
 
@@ -376,5 +411,6 @@ hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb) {
 }
 
 int regenLdsStack() { return REGEN_LDS_STACK; }
+int regenTop4() { return REGEN_TOP4; }
 
 }  // namespace pt

@@ -140,7 +140,12 @@ struct pt_ctx {
   bool pipe = false;                        // this context pipelines its megakernel frames
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
   bool gridShare = true;                    // frames in flight split the persistent grid (PT_GRID_SHARE=0: not)
-  int gridPct = 100;                        // % of residency the frames in flight split (PT_GRID_PCT)
+  // % of residency the frames in flight split (PT_GRID_PCT): 150 -- each frame's grid half again its
+  // equal share, so a frame finishing early leaves waves of the others ready to take its place --
+  // measured against 100 / 200 / 300 with the bench line as the driver runs it (20 frames from an
+  // idle GPU): c2 0.285 / 0.262 / 0.266 / 0.289 ms per frame (100 / 150 / 200 / 300), c4 0.413 /
+  // 0.360 / 0.367 / 0.385; 100 frames: c2 0.246 (100) vs 0.245 (200), c4 0.349 vs 0.332
+  int gridPct = 150;
   // the running mean updated tile by tile inside the frame kernels (renderKernel completeItem;
   // PT_KERNEL_MIX=1; off: mixKernel per frame on the caller's stream): per colour buffer and tile
   // the pixels written, per tile the lock word (2 x next frame to mix); valid from frame
@@ -1725,6 +1730,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
                                    &noOrder);
   // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
   if (regen && wide && ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE)) useFast = true;
+  if (regen && wide) p.scene.f4nTop = std::min(regenTop4(), ctx->f4nDev);  // its own LDS copy's size
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
@@ -1832,7 +1838,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // clock), appended per frame to $PT_WAVE_TRACE_FILE (tools/wave_trace.py)
   const size_t nTrace = (size_t)grid * (BLOCK / 64) * 6;
   unsigned long long* dTrace = nullptr;
-  if (!regen) {
+  {
     CK(hipMalloc(&dTrace, nTrace * sizeof(unsigned long long)));
     CK(hipMemsetAsync(dTrace, 0, nTrace * sizeof(unsigned long long), S));
   }

@@ -4,6 +4,7 @@
     python tools/tune.py --build wtrace:PT_WAVE_TRACE=1            # here
     PT_WAVE_TRACE_FILE=gpurun_out/w.bin python tools/tune.py --child wtrace --config c4 --frames 3 --warmup 0
     python tools/wave_trace.py gpurun_out/w.bin
+    python tools/wave_trace.py --regen gpurun_out/w.bin <waves per frame>   # the regen kernel's records
 
 Per frame: how long the frame lasted (first wave start to last wave end), how
 much of it the average wave was alive, the frame's tail (time from the median
@@ -14,7 +15,37 @@ import sys
 import numpy as np
 
 
+def regen(path, per=None):
+    """regenKernel records: start, end, tiles | last lone lane's pixel << 32, last successful claim,
+    loop iterations, iterations with at most 4 lanes active."""
+    raw = np.fromfile(path, dtype=np.uint64).reshape(-1, 6)
+    pix = (raw[:, 2] >> np.uint64(32)).astype(np.int64)
+    raw[:, 2] &= np.uint64(0xffffffff)
+    a = raw.astype(np.float64)
+    n = len(a)
+    per = per or n
+    us = lambda x: x / 100.0  # 100 MHz ticks -> us
+    for f in range(n // per):
+        r = a[f * per:(f + 1) * per]
+        px = pix[f * per:(f + 1) * per][r[:, 0] > 0]
+        r = r[r[:, 0] > 0]
+        t0, t1 = r[:, 0].min(), r[:, 1].max()
+        drained = r[:, 3].max()  # the last successful claim: every tile handed out
+        ends = np.sort(r[:, 1])
+        thin = r[:, 5] / np.maximum(r[:, 4], 1)
+        print(f"frame {f}: {len(r)} waves, frame {us(t1 - t0):7.1f} us, start spread {us(r[:, 0].max() - t0):6.1f}, "
+              f"queues drained at {us(drained - t0):7.1f}, tail after drain {us(t1 - drained):7.1f}, "
+              f"median end {us(np.median(ends) - t0):7.1f}, 99% end {us(ends[int(0.99 * len(ends))] - t0):7.1f}, "
+              f"tiles/wave {r[:, 2].mean():.1f}, iters/wave {r[:, 4].mean():.0f}, thin iters {thin.mean():.3f}")
+        last = np.argsort(-r[:, 1])[:5]
+        print("   last waves (end us, iters, thin iters, last lone pixel):",
+              ", ".join(f"{us(r[k, 1] - t0):.0f} {r[k, 4]:.0f} {r[k, 5]:.0f} ({px[k] >> 16},{px[k] & 0xffff})"
+                        for k in last))
+
+
 def main():
+    if sys.argv[1] == "--regen":
+        return regen(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else None)
     raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 6)
     at = (raw[:, 2] >> np.uint64(32)).astype(np.int64)  # (px << 16 | py) of the wave's longest tile
     raw[:, 2] &= np.uint64(0xffffffff)
