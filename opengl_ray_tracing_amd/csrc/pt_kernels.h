@@ -195,6 +195,7 @@ struct RenderParams {
   // PRIM_TILE (the tile's bin is over PT_BIN_CAP: the megakernel traces the tile's
   // packet); null = the megakernel traces its camera rays itself
   int2* primHit;
+  int zeroQueue;  // the camera-ray pass zeroes `queue` for the frame kernel after it (no memset)
   // band order (tileOrder null): items [0, staticItems) are dealt without atomics, wave w of
   // the grid taking w, w + waves, ...; the rest, staticItems + q * dynPerQueue + i, are
   // claimed from queue q as usual (staticItems 0: every item claimed)

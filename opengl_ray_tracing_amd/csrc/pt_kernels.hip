@@ -422,6 +422,8 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   __shared__ int s_idx[PT_PASS_BIN_CAP];
   const int w = blockIdx.x;
   const int lane = threadIdx.x;
+  if (p.zeroQueue && w == 0)  // the frame kernel's work-queue counters, zeroed for it (it runs next on this stream)
+    for (int q = lane; q < NUM_QUEUES; q += 64) p.queue[q * CTL_LINE_INTS] = 0;
   const int sub = p.shardSize >> 3;
   const int j = w / p.shardTiles, s = w - j * p.shardTiles;
   const int g = j * p.world + p.rank;

@@ -50,7 +50,11 @@ static constexpr int EV_RING = 64;
 #define PT_PIPE 8  // frames in flight (PT_PIPE_DEPTH overrides; capped by the hardware queues)
 #endif
 static constexpr int PIPE = MAX_SLOTS;      // most frames in flight
-static constexpr int COLS = MAX_SLOTS + 1;  // colour buffers (one more than the frames in flight)
+// colour buffers: a frame reuses the buffer of the frame 2 * depth + 1 back (the in-kernel running
+// mean's protocol: depth + 1 back), whose running-mean update is then long done -- with depth + 1 the
+// wait made a slot's next frame follow the running-mean update of the previous frame on another slot
+// (two cross-queue hops), and an N = 8 share of c2 kept only ~3 of its 8 frames in flight
+static constexpr int COLS = 2 * MAX_SLOTS + 1;
 static_assert(PT_PIPE >= 1 && PT_PIPE <= PIPE, "PT_PIPE: 1..MAX_SLOTS");
 static_assert(PIPE * NUM_QUEUES * CTL_LINE_INTS * 4 <= (int)CTL_STATS, "queue counters of every slot fit the control block");
 
@@ -146,6 +150,9 @@ struct pt_ctx {
   // idle GPU): c2 0.285 / 0.262 / 0.266 / 0.289 ms per frame (100 / 150 / 200 / 300), c4 0.413 /
   // 0.360 / 0.367 / 0.385; 100 frames: c2 0.246 (100) vs 0.245 (200), c4 0.349 vs 0.332
   int gridPct = 150;
+  // frame streams at the lowest stream priority (PT_SLOT_PRIORITY=1; measured slower: an N = 8 share
+  // of c2 0.065 -> 0.105 ms per frame)
+  bool slotPriority = false;
   // the running mean updated tile by tile inside the frame kernels (renderKernel completeItem;
   // PT_KERNEL_MIX=1; off: mixKernel per frame on the caller's stream): per colour buffer and tile
   // the pixels written, per tile the lock word (2 x next frame to mix); valid from frame
@@ -329,7 +336,17 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   hipDeviceProp_t prop;
   CKC(hipGetDeviceProperties(&prop, cfg->device_id));
   ctx->numCU = prop.multiProcessorCount;
-  CKC(hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking));
+  {
+    // the context's own stream (the running-mean updates' when the caller sets none) at the highest
+    // stream priority on request (PT_STREAM_PRIORITY=1; measured slower: an N = 8 share of c2
+    // 0.085 -> 0.124 ms per frame, c4 0.149 either way)
+    const char* e = std::getenv("PT_STREAM_PRIORITY");
+    int least = 0, greatest = 0;
+    if (e && std::atoi(e) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      CKC(hipStreamCreateWithPriority(&ctx->own, hipStreamNonBlocking, greatest));
+    else
+      CKC(hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking));
+  }
   ctx->stream = ctx->own;
   const size_t npix = (size_t)cfg->width * cfg->height;
   CKC(hipMalloc(&ctx->d_accum, npix * sizeof(float4)));
@@ -357,6 +374,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     if (const char* e = std::getenv("PT_PIPE_DEPTH")) ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
+    if (const char* e = std::getenv("PT_SLOT_PRIORITY")) ctx->slotPriority = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_KERNEL_MIX")) ctx->kernelMix = std::atoi(e) != 0;
     CKC(hipEventCreateWithFlags(&ctx->protoInit, hipEventDisableTiming));
     CKC(hipEventCreateWithFlags(&ctx->callerMark, hipEventDisableTiming));
@@ -1546,7 +1564,15 @@ static PackParams packParams(const pt_ctx* ctx, int rank, int world);
 // the slot streams (and their events) of depth D
 static int ensureSlots(pt_ctx* ctx, int D) {
   for (int k = 0; k < D; k++) {
-    if (!ctx->slotStream[k]) CK(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
+    if (!ctx->slotStream[k]) {
+      // the frames' streams at the lowest priority: the running-mean updates (on the caller's
+      // stream) and the caller's own work get the CUs first as the frames' waves retire
+      int least = 0, greatest = 0;
+      if (ctx->slotPriority && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        CK(hipStreamCreateWithPriority(&ctx->slotStream[k], hipStreamNonBlocking, least));
+      else
+        CK(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
+    }
     if (!ctx->kernelDone[k]) CK(hipEventCreateWithFlags(&ctx->kernelDone[k], hipEventDisableTiming));
   }
   return PT_OK;
@@ -1624,7 +1650,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   }
   const int D = piped ? ctx->pipeDepth : 1;
   const int slot = piped ? (int)(ctx->frameNo % (unsigned)D) : 0;
-  const int colIdx = piped ? (int)(ctx->frameNo % (unsigned)(D + 1)) : 0;
+  const bool protoFrame = piped && D > 1 && ctx->kernelMix && !regen;  // the in-kernel running mean (below)
+  const int nCol = protoFrame ? D + 1 : 2 * D + 1;
+  const int colIdx = piped ? (int)(ctx->frameNo % (unsigned)nCol) : 0;
   hipStream_t S = piped ? ctx->slotStream[slot] : ctx->stream;
   // every other slot's frame in flight has ended on S (the frames that read buffers
   // rebuilt below)
@@ -1663,15 +1691,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (rc) return rc;
   const size_t npix = (size_t)c.width * c.height;
   if (piped && !ctx->d_col[colIdx]) CK(hipMalloc(&ctx->d_col[colIdx], npix * sizeof(float4)));
-  // the colour buffer's previous frame (depth + 1 back) has been mixed -- and so, with work
-  // sharing, every frame before it has ended, including any that took this slot's previous
-  // frame's items: only then are the slot's queue counters, order list and camera-ray
-  // results reset for this frame
-  if (piped && ctx->frameNo >= (unsigned long long)(D + 1)) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
+  // the colour buffer's previous frame (nCol back) has been mixed (the slot's queue counters,
+  // order list and camera-ray results belong to its previous frame on this same stream)
+  if (piped && ctx->frameNo >= (unsigned long long)nCol) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
   int* queue = reinterpret_cast<int*>(ctx->d_ctl + CTL_QUEUES) + (size_t)slot * NUM_QUEUES * CTL_LINE_INTS;
-  // (the in-kernel running mean's frames zero them in frameVarKernel, right before the frame kernel)
-  if (!(piped && D > 1 && ctx->kernelMix && !regen))
-    CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   RenderParams p;
   std::memset(&p, 0, sizeof(p));
   p.scene = sceneView(ctx);
@@ -1797,7 +1820,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // frame, once the tile protocol's state is valid for it -- else, first, after every
   // earlier frame and the caller's stream's work so far (a cleared accumulation), the
   // state is reset on this frame's stream and every slot's next frame waits for that.
-  const bool proto = piped && D > 1 && ctx->kernelMix && !regen;
+  const bool proto = protoFrame;
   if (proto) {
     if (!ctx->d_tileDone) {
       CK(hipMalloc(&ctx->d_tileDone, (size_t)COLS * ctx->numItems * sizeof(int)));
@@ -1844,6 +1867,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   }
   p.waveTrace = dTrace;
 #endif
+  // the slot's work-queue counters zeroed for this frame: by the camera-ray pass (block 0), by
+  // frameVarKernel for the in-kernel running mean's frames, else by a memset
+  p.zeroQueue = p.primHit != nullptr;
+  if (!p.primHit && !proto) CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   CK(hipEventRecord(evb, S));
   if (p.primHit) CK(launchPrimary(p, S));
   if (proto) {  // its FrameVar for the earlier frames' waves that may mix its tiles; its queue counters zeroed
