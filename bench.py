@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="rehearsal: every rank on device 0")
+    ap.add_argument("--gather", choices=["display", "accum"], default="display",
+                    help="--shard tiles: per frame, gather the displayed frame (RGB8, 3 B/pixel; the running "
+                         "means gathered once after the run) or the running means (3 f32 per pixel)")
     ap.add_argument("--shard", choices=["samples", "tiles"], default="tiles",
                     help="N > 1: sample-parallel full frames (weak) or screen-tile shards of one frame (strong)")
     return ap.parse_args()
@@ -132,7 +135,7 @@ def main():
     gather = combine = None
     if tiles:
         from opengl_ray_tracing_amd.distributed import FrameGather
-        gather = FrameGather(r, rank, n, f"cuda:{local}")
+        gather = FrameGather(r, rank, n, f"cuda:{local}", mode=args.gather)
     elif n > 1:
         from opengl_ray_tracing_amd.distributed import SampleReduce
         combine = SampleReduce(r, rank, n, f"cuda:{local}")
@@ -200,6 +203,10 @@ def main():
             ss = rs.stats()
             serial_ms = ss.kernel_ms_total / max(ss.launches, 1)
     combined_finite = None
+    if gather is not None and args.gather == "display":  # the running means to rank 0, once (not timed)
+        gather.gather_accum()
+        if rank == 0:
+            combined_finite = bool(np.isfinite(r.accum()).all())
     if combine is not None:  # the ranks' running means -> one image on rank 0 (after the timed steps)
         img = combine()
         torch.cuda.synchronize()
@@ -265,7 +272,10 @@ def main():
                        "traversal_tree": "runtime (checked against uploaded)" if st.runtime_tree else "uploaded",
                        "frame_kernel": "path regeneration" if st.regen else "lock-step megakernel",
                        "waves_per_simd": st.waves_per_simd, "frames_in_flight": st.frames_in_flight,
-                       "parallelism": (f"screen-tile x{n}" + (" + RCCL gather per frame" if n > 1 else ""))
+                       "parallelism": (f"screen-tile x{n}" + ((" + RCCL gather per frame of the displayed frame "
+                                                               "(RGB8)" if args.gather == "display" else
+                                                               " + RCCL gather per frame of the running means (f32)")
+                                                              if n > 1 else ""))
                        if args.shard == "tiles" else
                        (f"sample-parallel x{n}" + (" (RCCL reduce of the running means after the run)"
                                                    if n > 1 else ""))},

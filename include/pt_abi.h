@@ -26,9 +26,10 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 4  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
+#define PT_ABI_VERSION 5  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
                              3: scene-upload fields at the end of pt_frame_stats, pt_build_bvh_device;
-                             4: BASIC shapes as doubles, its double image, the replayed random stream */
+                             4: BASIC shapes as doubles, its double image, the replayed random stream;
+                             5: the displayed frame of a screen-tile split (pt_display_*) */
 
 /* error codes */
 #define PT_OK 0
@@ -226,6 +227,21 @@ int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out);
 int pt_owned_pixel_count(pt_ctx* ctx, int rank, int world, int64_t* count);
 int pt_pack_owned(pt_ctx* ctx, void* dpacked);
 int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked);
+
+/* The displayed frame (pass3.fsh:14-24 drawn into the 8-bit GLUT_RGBA window,
+ * ImportanceSampling_LowDiscrepancySequence/main.cpp:706,747): tonemap (and gamma > 0)
+ * of the accumulation, stored as round(clamp(x, 0, 1) * 255) per channel, alpha 255.
+ * A screen-tile split presents every frame from 3 bytes per pixel instead of the
+ * accumulation's 12: each rank packs its owned pixels' display values
+ * (pt_display_pack: pt_owned_pixel_count slots of 3 u8, packed order as pt_pack_owned),
+ * the caller moves them to rank 0 (RCCL gather over xGMI), and rank 0 writes its own
+ * tiles (pt_display_own) and the other ranks' (pt_display_unpack: dpacked[k] = rank k's
+ * packed buffer for k = 1..world-1, world <= 16, one launch) into one width x height
+ * RGBA8 device image. With tile_world 1, pt_display_own writes every pixel. All on the
+ * context's current stream, after the frames rendered so far; device pointers. */
+int pt_display_pack(pt_ctx* ctx, float limit, float gamma, void* dpacked);
+int pt_display_own(pt_ctx* ctx, float limit, float gamma, void* dimage);
+int pt_display_unpack(pt_ctx* ctx, int world, const void* const* dpacked, void* dimage);
 
 /* Stream interop: render on the caller's HIP stream (e.g. torch's current
  * stream). NULL restores the context's own stream. */

@@ -13,7 +13,7 @@ from . import _build
 
 _lib = None
 
-ABI_VERSION = 4  # include/pt_abi.h PT_ABI_VERSION
+ABI_VERSION = 5  # include/pt_abi.h PT_ABI_VERSION
 c_float_p = C.POINTER(C.c_float)
 c_double_p = C.POINTER(C.c_double)
 c_int_p = C.POINTER(C.c_int)
@@ -77,6 +77,9 @@ SIGNATURES = {
     "pt_owned_pixel_count": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int64)]),
     "pt_pack_owned": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pt_unpack_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "pt_display_pack": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_void_p]),
+    "pt_display_own": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_void_p]),
+    "pt_display_unpack": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.c_void_p]),
     "pt_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pt_synchronize": (C.c_int, [C.c_void_p]),
     "pt_get_stats": (C.c_int, [C.c_void_p, C.POINTER(PtFrameStats)]),

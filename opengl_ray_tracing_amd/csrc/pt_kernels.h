@@ -263,6 +263,14 @@ struct PackParams {
   int width, height, shardSize, shardsX, rank, world;
   long count;
 };
+// the displayed frame's unpack on rank 0 (pt_display_unpack): ranks 1..world-1's packed RGB8
+// buffers (null: skipped) and slot counts; base's rank / count are per rank
+constexpr int DISPLAY_MAX_WORLD = 16;
+struct DisplayUnpack {
+  PackParams base;
+  const uint8_t* src[DISPLAY_MAX_WORLD];
+  long count[DISPLAY_MAX_WORLD];
+};
 
 // camera-ray bins of one camera (pt_primary.hip), device buffers owned by the context
 #ifndef PT_BIN_CAP
@@ -347,6 +355,11 @@ hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, fl
 constexpr int PACK_F = 3;
 hipError_t launchPack(const PackParams& p, const float4* accum, float* packed, hipStream_t s);
 hipError_t launchFmath(int fn, const float* x, const float* y, int n, float* out, hipStream_t s);
+hipError_t launchDisplayPack(const PackParams& p, const float4* accum, float limit, float gamma, uint8_t* packed,
+                             hipStream_t s);
+hipError_t launchDisplayOwn(const PackParams& p, const float4* accum, float limit, float gamma, uchar4* image,
+                            hipStream_t s);
+hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image, hipStream_t s);
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s);
 // the running-mean update of a pipelined frame over the rank's owned pixels (PackParams
 // mapping): accum = mix(accum, col, 1 / (frameCounter + 1)) (IS:868-871, pass2.fsh:15)

@@ -1117,10 +1117,7 @@ __global__ __launch_bounds__(BLOCK) void traceKernel(TraceParams p) {
 
 // ------------------------------------------------------------ epilogues
 // pass3.fsh:14-24 tonemap (+ optional gamma, commented out in the reference)
-__global__ void tonemapKernel(const float4* accum, float* rgb, int n, float limit, float gamma) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float4 c = accum[i];
+__device__ __forceinline__ V3 tonemapPixel(float4 c, float limit, float gamma) {
   float lum = 0.3f * c.x + 0.6f * c.y + 0.1f * c.z;
   float s = 1.0f / (1.0f + lum / limit);
   float r = c.x * s, g = c.y * s, b = c.z * s;
@@ -1129,9 +1126,22 @@ __global__ void tonemapKernel(const float4* accum, float* rgb, int n, float limi
     g = ptm_powf(g, 1.0f / gamma);
     b = ptm_powf(b, 1.0f / gamma);
   }
-  rgb[3 * i] = r;
-  rgb[3 * i + 1] = g;
-  rgb[3 * i + 2] = b;
+  return v3(r, g, b);
+}
+__global__ void tonemapKernel(const float4* accum, float* rgb, int n, float limit, float gamma) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const V3 c = tonemapPixel(accum[i], limit, gamma);
+  rgb[3 * i] = c.x;
+  rgb[3 * i + 1] = c.y;
+  rgb[3 * i + 2] = c.z;
+}
+// pass3's fragColor as the GLUT_RGBA window stores it (OpenglRayTracing/main.cpp glutInitDisplayMode,
+// an 8-bit unsigned-normalised framebuffer): round(clamp(x, 0, 1) * 255), as one fused multiply-add
+// (NaN -> 0)
+__device__ __forceinline__ uint32_t unorm8(float x) {
+  const float c = fminf(fmaxf(x, 0.0f), 1.0f);
+  return (uint32_t)__builtin_fmaf(c, 255.0f, 0.5f);
 }
 
 // pack (unpack) the pixels of shard tiles t % world == rank in (tile, row, col) order
@@ -1162,6 +1172,46 @@ __global__ void unpackKernel(PackParams p, float4* accum, const float* packed) {
   int px, py;
   if (packedPixel(p, k, px, py))
     accum[(size_t)py * p.width + px] = make_float4(packed[3 * k], packed[3 * k + 1], packed[3 * k + 2], 1.0f);
+}
+
+// The displayed frame (pass3 into the 8-bit window) of a screen-tile split: each rank packs its
+// own tiles' display values (3 bytes per pixel, packed order) and rank 0 writes its own tiles and
+// unpacks every other rank's into one RGBA8 image -- a quarter of the f32 gather's bytes over xGMI.
+__global__ void displayPackKernel(PackParams p, const float4* accum, float limit, float gamma, uint8_t* packed) {
+  long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= p.count) return;
+  int px, py;
+  uint32_t r = 0, g = 0, b = 0;
+  if (packedPixel(p, k, px, py)) {
+    const V3 c = tonemapPixel(accum[(size_t)py * p.width + px], limit, gamma);
+    r = unorm8(c.x), g = unorm8(c.y), b = unorm8(c.z);
+  }
+  packed[3 * k] = (uint8_t)r;
+  packed[3 * k + 1] = (uint8_t)g;
+  packed[3 * k + 2] = (uint8_t)b;
+}
+__global__ void displayOwnKernel(PackParams p, const float4* accum, float limit, float gamma, uchar4* image) {
+  long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= p.count) return;
+  int px, py;
+  if (!packedPixel(p, k, px, py)) return;
+  const size_t i = (size_t)py * p.width + px;
+  const V3 c = tonemapPixel(accum[i], limit, gamma);
+  image[i] = make_uchar4((uint8_t)unorm8(c.x), (uint8_t)unorm8(c.y), (uint8_t)unorm8(c.z), 255);
+}
+// blockIdx.y = rank - 1 of ranks 1..world-1 (their packed buffers in d.src)
+__global__ void displayUnpackKernel(DisplayUnpack d, uchar4* image) {
+  const int rank = blockIdx.y + 1;
+  const uint8_t* src = d.src[rank];
+  if (!src) return;
+  PackParams p = d.base;
+  p.rank = rank;
+  p.count = d.count[rank];
+  long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= p.count) return;
+  int px, py;
+  if (packedPixel(p, k, px, py))
+    image[(size_t)py * p.width + px] = make_uchar4(src[3 * k], src[3 * k + 1], src[3 * k + 2], 255);
 }
 
 // the running mean of a pipelined frame (accumulate's update, deferred to frame order)
@@ -1287,6 +1337,28 @@ __global__ void frameVarKernel(FrameVar v, FrameVar* dst, int* queue) {
 }
 hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, int* queue, hipStream_t s) {
   hipLaunchKernelGGL(frameVarKernel, dim3(1), dim3(64), 0, s, v, dst, queue);
+  return hipGetLastError();
+}
+hipError_t launchDisplayPack(const PackParams& p, const float4* accum, float limit, float gamma, uint8_t* packed,
+                             hipStream_t s) {
+  if (p.count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(displayPackKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, limit,
+                     gamma, packed);
+  return hipGetLastError();
+}
+hipError_t launchDisplayOwn(const PackParams& p, const float4* accum, float limit, float gamma, uchar4* image,
+                            hipStream_t s) {
+  if (p.count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(displayOwnKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, limit,
+                     gamma, image);
+  return hipGetLastError();
+}
+hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image, hipStream_t s) {
+  long most = 0;
+  for (int k = 1; k < world; k++) most = d.count[k] > most ? d.count[k] : most;
+  if (world < 2 || most <= 0) return hipSuccess;
+  hipLaunchKernelGGL(displayUnpackKernel, dim3((unsigned)((most + 255) / 256), (unsigned)(world - 1)), dim3(256), 0, s,
+                     d, image);
   return hipGetLastError();
 }
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s) {

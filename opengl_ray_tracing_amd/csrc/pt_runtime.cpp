@@ -2129,6 +2129,41 @@ int pt_pack_owned(pt_ctx* ctx, void* dpacked) {
   return PT_OK;
 }
 
+int pt_display_pack(pt_ctx* ctx, float limit, float gamma, void* dpacked) {
+  if (!ctx || !dpacked || !(limit > 0.0f)) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
+  if (int rc = joinPipe(ctx)) return rc;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  PackParams p = packParams(ctx, ctx->cfg.tile_rank, ctx->cfg.tile_world);
+  CK(launchDisplayPack(p, ctx->d_accum, limit, gamma, reinterpret_cast<uint8_t*>(dpacked), ctx->stream));
+  return PT_OK;
+}
+
+int pt_display_own(pt_ctx* ctx, float limit, float gamma, void* dimage) {
+  if (!ctx || !dimage || !(limit > 0.0f)) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
+  if (int rc = joinPipe(ctx)) return rc;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  PackParams p = packParams(ctx, ctx->cfg.tile_rank, ctx->cfg.tile_world);
+  CK(launchDisplayOwn(p, ctx->d_accum, limit, gamma, reinterpret_cast<uchar4*>(dimage), ctx->stream));
+  return PT_OK;
+}
+
+int pt_display_unpack(pt_ctx* ctx, int world, const void* const* dpacked, void* dimage) {
+  if (!ctx || !dpacked || !dimage || world < 1 || world > DISPLAY_MAX_WORLD) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
+  CK(hipSetDevice(ctx->cfg.device_id));
+  DisplayUnpack d;
+  std::memset(&d, 0, sizeof(d));
+  d.base = packParams(ctx, 0, world);
+  for (int k = 1; k < world; k++) {
+    d.src[k] = reinterpret_cast<const uint8_t*>(dpacked[k]);
+    d.count[k] = packParams(ctx, k, world).count;
+  }
+  CK(launchDisplayUnpack(d, world, reinterpret_cast<uchar4*>(dimage), ctx->stream));
+  return PT_OK;
+}
+
 int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked) {
   if (!ctx || !dpacked || world < 1 || rank < 0 || rank >= world) return PT_E_INVALID;
   if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");

@@ -65,27 +65,40 @@ def unpack(accum: np.ndarray, packed: np.ndarray, rank: int, world: int, shard: 
 
 
 class FrameGather:
-    """RCCL gather of every rank's shard of a Renderer's accumulation to rank 0.
+    """RCCL gather of every rank's screen-tile shard to rank 0, once per frame.
 
-    Device buffers are torch tensors (torch is the allocator/collective
-    plumbing here). The renderer runs on torch's current stream; each call
-    packs the frame just rendered there into one of two send buffers and runs
-    the gather -- and on rank 0 the unpack into its accumulation -- on a
-    communication stream, so frame f's gather overlaps frame f+1's render
-    (rank 0's render writes only its own tiles, the unpack only the others').
-    A send buffer is packed again only after its previous gather finished.
-    `synchronize()` (or the device-wide synchronise a caller does anyway)
-    completes the last frame's gather; rank 0's accumulation then holds the
-    whole frame, bit-identical to a single-GPU render. `overlap=False` runs
-    everything on the render stream.
+    Two things to gather (`mode`):
+
+    * "display" -- the frame as presented (pass3.fsh tonemap into the reference's 8-bit
+      GLUT_RGBA window, ImportanceSampling_LowDiscrepancySequence/main.cpp:706,747): every
+      rank packs its tiles' display values (3 bytes per pixel, pt_display_pack), rank 0
+      writes its own tiles and unpacks the others' into an H x W x 4 u8 image
+      (pt_display_own / pt_display_unpack). A quarter of the accumulation's bytes cross
+      xGMI per frame; each rank's running mean stays with it (`gather_accum()` brings the
+      whole accumulation to rank 0 when it is wanted, bit-identical to a 1-GPU render).
+    * "accum" -- the running mean itself (3 f32 per pixel, pt_pack_owned / pt_unpack_rank)
+      into rank 0's accumulation every frame.
+
+    Device buffers are torch tensors (torch is the allocator/collective plumbing here).
+    The renderer runs on a torch stream of its own; each call packs the frame just
+    rendered into one of two send buffers and runs the gather -- and on rank 0 the
+    unpack -- on a communication stream, so frame f's gather overlaps frame f+1's render
+    (rank 0's render writes only its own tiles, the unpack only the others'). A send
+    buffer (and, in display mode, an image) is written again only after its previous
+    gather finished. `synchronize()` completes the last frame's gather. `overlap=False`
+    runs everything on the render stream.
     """
 
-    def __init__(self, renderer, rank: int, world: int, device, overlap: bool = True):
+    def __init__(self, renderer, rank: int, world: int, device, overlap: bool = True, mode: str = "accum",
+                 limit: float = 1.5, gamma: float = 0.0):
         import torch
         import torch.distributed as dist
 
+        if mode not in ("accum", "display"):
+            raise ValueError(f"mode {mode!r}")
         self.torch, self.dist = torch, dist
-        self.r, self.rank, self.world = renderer, rank, world
+        self.r, self.rank, self.world, self.device = renderer, rank, world, device
+        self.mode, self.limit, self.gamma = mode, float(limit), float(gamma)
         counts = [renderer.owned_pixel_count(k, world) for k in range(world)]
         self.maxc = max(counts)
         self.overlap = overlap and not _staged()
@@ -94,46 +107,99 @@ class FrameGather:
         self.render_stream = torch.cuda.Stream(device)
         self.comm_stream = torch.cuda.Stream(device) if self.overlap else self.render_stream
         nbuf = 2 if self.overlap else 1
-        # packed slots: 3 f32 (r, g, b; pt_pack_owned), 12 bytes per pixel over xGMI
-        self.send = [torch.zeros((self.maxc, 3), dtype=torch.float32, device=device) for _ in range(nbuf)]
-        self.sent = [None] * nbuf  # event: the buffer's last gather has completed
-        self.recv = [torch.zeros((self.maxc, 3), dtype=torch.float32, device=device) for _ in range(world)] \
+        if mode == "display":  # packed slots: 3 u8 (r, g, b of the displayed pixel)
+            shape, dtype = (self.maxc * 3,), torch.uint8
+        else:  # packed slots: 3 f32 (r, g, b; pt_pack_owned), 12 bytes per pixel over xGMI
+            shape, dtype = (self.maxc, 3), torch.float32
+        self.send = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
+        self.recv = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(world)] \
             if rank == 0 else None
+        self.images = [torch.zeros((renderer.height, renderer.width, 4), dtype=torch.uint8, device=device)
+                       for _ in range(nbuf)] if (mode == "display" and rank == 0) else None
+        self._recv_ptrs = [0] + [t.data_ptr() for t in self.recv[1:]] if self.recv is not None else None
+        self.packed = [torch.cuda.Event() for _ in range(nbuf)]
+        self.done = [torch.cuda.Event() for _ in range(nbuf)]
+        self.used = [False] * nbuf  # the buffer's done event has been recorded
         self.k = 0
+        self.last = None  # index of the image holding the last presented frame (rank 0, display mode)
         renderer.set_stream(self.render_stream.cuda_stream)
+
+    @property
+    def image(self):
+        """Rank 0, display mode: the last presented frame (H x W x 4 u8, device), complete
+        once its gather has (synchronize(), or the comm stream's done event)."""
+        return None if self.images is None or self.last is None else self.images[self.last]
+
+    def _pack(self, i):
+        if self.mode == "display":
+            if self.rank == 0:
+                self.r.display_own(self.images[i].data_ptr(), self.limit, self.gamma)
+            else:
+                self.r.display_pack(self.send[i].data_ptr(), self.limit, self.gamma)
+        else:
+            self.r.pack_owned(self.send[i].data_ptr())
+
+    def _unpack(self, i):
+        if self.mode == "display":
+            self.r.display_unpack(self.world, self._recv_ptrs, self.images[i].data_ptr())
+        else:
+            for k in range(1, self.world):
+                self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
 
     def __call__(self):
         torch, dist = self.torch, self.dist
         i = self.k % len(self.send)
         self.k += 1
-        buf = self.send[i]
-        if self.sent[i] is not None:
-            self.render_stream.wait_event(self.sent[i])
-        self.r.pack_owned(buf.data_ptr())  # on the render stream, after the frame
+        if self.used[i]:
+            self.render_stream.wait_event(self.done[i])
+        self._pack(i)  # on the render stream, after the frame
+        if self.mode == "display" and self.rank == 0:
+            self.last = i
         if _staged():  # gloo rehearsal: the collective on host copies, ordered after the pack
             with torch.cuda.stream(self.render_stream):
-                host = buf.cpu()
+                host = self.send[i].cpu()
                 recv = [torch.zeros_like(host) for _ in range(self.world)] if self.rank == 0 else None
                 dist.gather(host, gather_list=recv, dst=0)
                 if self.rank == 0:
                     for t, h in zip(self.recv, recv):
                         t.copy_(h)
-                    for k in range(1, self.world):
-                        self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
+                    self._unpack(i)
             return
-        packed = torch.cuda.Event()
-        packed.record(self.render_stream)
+        self.packed[i].record(self.render_stream)
         with torch.cuda.stream(self.comm_stream):
-            self.comm_stream.wait_event(packed)
-            dist.gather(buf, gather_list=self.recv, dst=0)
+            self.comm_stream.wait_event(self.packed[i])
+            dist.gather(self.send[i], gather_list=self.recv, dst=0)
             if self.rank == 0:
                 self.r.set_stream(self.comm_stream.cuda_stream)
-                for k in range(1, self.world):
-                    self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
+                self._unpack(i)
                 self.r.set_stream(self.render_stream.cuda_stream)
-            done = torch.cuda.Event()
-            done.record(self.comm_stream)
-        self.sent[i] = done
+            self.done[i].record(self.comm_stream)
+        self.used[i] = True
+
+    def gather_accum(self):
+        """Bring every rank's running mean to rank 0's accumulation (3 f32 per pixel, once,
+        synchronous): rank 0 then holds the whole accumulation, bit-identical to a 1-GPU
+        render. Collective: every rank calls it."""
+        torch, dist = self.torch, self.dist
+        self.synchronize()
+        buf = torch.zeros((self.maxc, 3), dtype=torch.float32, device=self.device)
+        self.r.pack_owned(buf.data_ptr())
+        self.render_stream.synchronize()
+        recv = [torch.zeros_like(buf) for _ in range(self.world)] if self.rank == 0 else None
+        if _staged():
+            host = buf.cpu()
+            hrecv = [torch.zeros_like(host) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(host, gather_list=hrecv, dst=0)
+            if self.rank == 0:
+                for t, h in zip(recv, hrecv):
+                    t.copy_(h)
+        else:
+            with torch.cuda.stream(self.render_stream):
+                dist.gather(buf, gather_list=recv, dst=0)
+        if self.rank == 0:
+            for k in range(1, self.world):
+                self.r.unpack_rank(k, self.world, recv[k].data_ptr())
+        self.render_stream.synchronize()
 
     def synchronize(self):
         self.comm_stream.synchronize()

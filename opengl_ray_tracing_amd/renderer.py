@@ -254,6 +254,19 @@ class Renderer:
     def unpack_rank(self, rank: int, world: int, dptr: int):
         self._ck(self._lib.pt_unpack_rank(self._h, int(rank), int(world), C.c_void_p(dptr)), "pt_unpack_rank")
 
+    def display_pack(self, dptr: int, limit: float = 1.5, gamma: float = 0.0):
+        """This rank's owned pixels of the displayed frame (pass3 into an 8-bit window), 3 u8 each."""
+        self._ck(self._lib.pt_display_pack(self._h, float(limit), float(gamma), C.c_void_p(dptr)), "pt_display_pack")
+
+    def display_own(self, dimage: int, limit: float = 1.5, gamma: float = 0.0):
+        """This rank's tiles (every pixel when tile_world is 1) of the displayed frame into an H x W x 4 u8 image."""
+        self._ck(self._lib.pt_display_own(self._h, float(limit), float(gamma), C.c_void_p(dimage)), "pt_display_own")
+
+    def display_unpack(self, world: int, dpacked, dimage: int):
+        """Ranks 1..world-1's packed display pixels (device pointers, entry 0 ignored) into the image."""
+        arr = (C.c_void_p * world)(*[C.c_void_p(int(x)) if x else C.c_void_p() for x in dpacked])
+        self._ck(self._lib.pt_display_unpack(self._h, int(world), arr, C.c_void_p(dimage)), "pt_display_unpack")
+
     def set_stream(self, stream_ptr: int | None):
         self._ck(self._lib.pt_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None), "pt_set_stream")
 

@@ -169,6 +169,76 @@ def test_tonemap_matches_pass3():
     assert np.allclose(tg, np.power(want, 1 / 2.2), rtol=1e-5, atol=1e-6)
 
 
+def _unorm8(x):
+    """round(clamp(x, 0, 1) * 255) as the display kernels compute it: one fused multiply-add
+    (exact in f64, then one rounding to f32), truncated."""
+    c = np.clip(np.nan_to_num(x.astype(np.float32), nan=0.0), 0, 1).astype(np.float64)
+    return np.floor((c * 255.0 + 0.5).astype(np.float32)).astype(np.uint8)
+
+
+@pytest.mark.parametrize("gamma", [0.0, 2.2])
+def test_display_frame_is_pass3_in_an_8bit_window(gamma):
+    """pt_display_own of an unsplit context: every pixel's pass3 tonemap (the GPU's own f32
+    tonemap, pt_tonemap) stored as an 8-bit unsigned-normalised RGBA pixel, alpha 255."""
+    import torch
+    cfg, tris, nodes, hdr = scenes.build_config("c2")
+    eye, rot = orbit_camera(*cfg.camera)
+    with Renderer(320, 180, "lambert") as r:
+        r.upload_scene(tris, nodes)
+        r.upload_env(hdr)
+        for f in range(2):
+            r.render_frame(eye, rot, f)
+        t = r.tonemap(1.5, gamma)
+        img = torch.zeros((180, 320, 4), dtype=torch.uint8, device="cuda:0")
+        r.display_own(img.data_ptr(), 1.5, gamma)
+        r.synchronize()
+    got = img.cpu().numpy()
+    assert np.array_equal(got[..., :3], _unorm8(t)) and np.all(got[..., 3] == 255)
+
+
+def test_display_split_reassembles_the_frame():
+    """Three tile ranks on one device: each packs its display pixels (3 u8 per owned slot), rank 0
+    writes its own tiles and unpacks the other two in one launch -- the same RGBA8 frame as an
+    unsplit context; rank 0's own tiles alone leave the others' pixels untouched."""
+    import torch
+    cfg, tris, nodes, hdr = scenes.build_config("c2")
+    eye, rot = orbit_camera(*cfg.camera)
+    W, H, world = 200, 130, 3
+    full = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")
+    with Renderer(W, H, "lambert") as r:
+        r.upload_scene(tris, nodes)
+        r.upload_env(hdr)
+        r.render_frame(eye, rot, 0)
+        r.display_own(full.data_ptr())
+        r.synchronize()
+    rs = [Renderer(W, H, "lambert", tile_rank=k, tile_world=world) for k in range(world)]
+    try:
+        packed = []
+        for k, rr in enumerate(rs):
+            rr.upload_scene(tris, nodes)
+            rr.upload_env(hdr)
+            rr.render_frame(eye, rot, 0)
+            buf = torch.zeros(rr.owned_pixel_count() * 3, dtype=torch.uint8, device="cuda:0")
+            rr.display_pack(buf.data_ptr())
+            rr.synchronize()
+            packed.append(buf)
+        img = torch.full((H, W, 4), 7, dtype=torch.uint8, device="cuda:0")
+        rs[0].display_own(img.data_ptr())
+        rs[0].synchronize()
+        own_only = img.cpu().numpy()
+        rs[0].display_unpack(world, [0] + [b.data_ptr() for b in packed[1:]], img.data_ptr())
+        rs[0].synchronize()
+    finally:
+        for rr in rs:
+            rr.close()
+    want = full.cpu().numpy()
+    assert np.array_equal(img.cpu().numpy(), want)
+    mine = np.zeros((H, W), bool)
+    p = D.owned_pixels(W, H, 0, world)
+    mine[p[:, 1], p[:, 0]] = True
+    assert np.array_equal(own_only[mine], want[mine]) and np.all(own_only[~mine] == 7)
+
+
 def test_error_paths():
     with Renderer(16, 16) as r:
         with pytest.raises(_native.PtError):
