@@ -122,6 +122,7 @@ class FrameGather:
         self.used = [False] * nbuf  # the buffer's done event has been recorded
         self.k = 0
         self.last = None  # index of the image holding the last presented frame (rank 0, display mode)
+        torch.cuda.current_stream(device).synchronize()  # the buffers' fills, before the other streams use them
         renderer.set_stream(self.render_stream.cuda_stream)
 
     @property
@@ -182,23 +183,22 @@ class FrameGather:
         render. Collective: every rank calls it."""
         torch, dist = self.torch, self.dist
         self.synchronize()
-        buf = torch.zeros((self.maxc, 3), dtype=torch.float32, device=self.device)
-        self.r.pack_owned(buf.data_ptr())
-        self.render_stream.synchronize()
-        recv = [torch.zeros_like(buf) for _ in range(self.world)] if self.rank == 0 else None
-        if _staged():
-            host = buf.cpu()
-            hrecv = [torch.zeros_like(host) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(host, gather_list=hrecv, dst=0)
-            if self.rank == 0:
-                for t, h in zip(recv, hrecv):
-                    t.copy_(h)
-        else:
-            with torch.cuda.stream(self.render_stream):
+        with torch.cuda.stream(self.render_stream):  # every allocation, copy and kernel in one stream order
+            buf = torch.zeros((self.maxc, 3), dtype=torch.float32, device=self.device)
+            self.r.pack_owned(buf.data_ptr())
+            recv = [torch.zeros_like(buf) for _ in range(self.world)] if self.rank == 0 else None
+            if _staged():
+                host = buf.cpu()
+                hrecv = [torch.zeros_like(host) for _ in range(self.world)] if self.rank == 0 else None
+                dist.gather(host, gather_list=hrecv, dst=0)
+                if self.rank == 0:
+                    for t, h in zip(recv, hrecv):
+                        t.copy_(h)
+            else:
                 dist.gather(buf, gather_list=recv, dst=0)
-        if self.rank == 0:
-            for k in range(1, self.world):
-                self.r.unpack_rank(k, self.world, recv[k].data_ptr())
+            if self.rank == 0:
+                for k in range(1, self.world):
+                    self.r.unpack_rank(k, self.world, recv[k].data_ptr())
         self.render_stream.synchronize()
 
     def synchronize(self):

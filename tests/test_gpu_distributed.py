@@ -83,7 +83,13 @@ def _tile_worker(rank, world, port, backend, q, mode):
                       "got", got[bad[0][0], bad[0][1]], "ref", ref[bad[0][0], bad[0][1]], flush=True)
             exact = bool(np.array_equal(got, ref))
             if mode == "display":
-                exact = exact and bool(np.array_equal(shown, ref_img)) and bool(np.all(shown[..., 3] == 255))
+                img_ok = bool(np.array_equal(shown, ref_img)) and bool(np.all(shown[..., 3] == 255))
+                if not img_ok:
+                    bad = np.argwhere(np.any(shown != ref_img, axis=-1))
+                    print("display mismatch", len(bad), "first", bad[:3].tolist(), shown[tuple(bad[0])],
+                          ref_img[tuple(bad[0])], flush=True)
+                print("accum exact", exact, "image exact", img_ok, flush=True)
+                exact = exact and img_ok
             q.put((exact, int(rays.item()) == ref_rays, g.overlap))
         r.close()
     finally:
