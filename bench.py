@@ -98,6 +98,9 @@ def main():
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
     n = world
 
+    if os.environ.get("PT_VARIANT"):  # A/B of an in-tree tuning build (tools/tune.py --build); not a default run
+        from opengl_ray_tracing_amd import _native
+        _native.use_variant(os.environ["PT_VARIANT"])
     from opengl_ray_tracing_amd import FLAG_COUNT_FETCHES, Renderer, orbit_camera, scenes
 
     cfg, tris, nodes, hdr = scenes.build_config(args.config, args.builder)

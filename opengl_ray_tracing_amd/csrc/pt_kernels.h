@@ -36,9 +36,15 @@ constexpr int WIDE_WAVES = 3;
 #define PT_REGEN_YIELD_REL 0  // 1: PT_REGEN_YIELD counts 64ths of the lanes walking together, not lanes
 #endif
 #ifndef PT_WIDE_REGEN_WAVES
-#define PT_WIDE_REGEN_WAVES 4
+#define PT_WIDE_REGEN_WAVES 4  // MIS
+#endif
+// the uniform integrators' (Lambert, Disney) variant: 3 waves per SIMD leave its 163 VGPRs unspilled
+// (4 waves: 128 VGPRs, 59 spilled): c2 0.241 -> 0.235 ms per frame (5 waves: 0.313)
+#ifndef PT_WIDE_REGEN_WAVES_U
+#define PT_WIDE_REGEN_WAVES_U 3
 #endif
 constexpr int WIDE_REGEN_WAVES = PT_WIDE_REGEN_WAVES;
+constexpr int wideRegenWaves(int integrator) { return integrator == 2 ? PT_WIDE_REGEN_WAVES : PT_WIDE_REGEN_WAVES_U; }
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
@@ -347,7 +353,7 @@ hipError_t launchPrimary(const RenderParams& p, hipStream_t s);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool wide = false);
 hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb);
 int regenLdsStack();
-int regenTop4();  // 4-wide nodes the wide regen kernel stages in LDS (PT_REGEN_TOP4)
+int regenTop4(int integrator);  // 4-wide nodes the wide regen kernel stages in LDS (PT_REGEN_TOP4[_3])
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s);

@@ -53,7 +53,12 @@ constexpr int REGEN_LDS_STACK = PT_REGEN_LDS_STACK;
 #ifndef PT_REGEN_TOP4
 #define PT_REGEN_TOP4 128
 #endif
-constexpr int REGEN_TOP4 = PT_REGEN_TOP4;
+// ... and at 3 waves per SIMD (the uniform integrators' variant): 128 too (c2 0.235 ms per frame;
+// 256, which 3 blocks per CU would fit, 0.240)
+#ifndef PT_REGEN_TOP4_3
+#define PT_REGEN_TOP4_3 128
+#endif
+constexpr int regenTop4W(int waves) { return waves == 3 ? PT_REGEN_TOP4_3 : PT_REGEN_TOP4; }
 
 enum : int { K_NONE = 0, K_PRIMARY = 1, K_BOUNCE = 2, K_SHADOW = 3 };
 
@@ -250,7 +255,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   st.reset();
   // the top of the uploaded tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
-  constexpr int TOPF4 = (W4 && REGEN_TOP4 * W4_F4 > LDS_NODES * 4) ? REGEN_TOP4 * W4_F4 : LDS_NODES * 4;
+  constexpr int TOP4 = regenTop4W(WAVES);
+  constexpr int TOPF4 = (W4 && TOP4 * W4_F4 > LDS_NODES * 4) ? TOP4 * W4_F4 : LDS_NODES * 4;
   __shared__ float4 s_nodes[TOPF4];
   {
     const bool w4 = W4 && p.scene.fast;
@@ -385,13 +391,13 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
 
 template <int I>
 static const void* regenFn(bool cull, bool wide) {
-  if (wide) return (const void*)regenKernel<I, true, WIDE_REGEN_WAVES, true>;
+  if (wide) return (const void*)regenKernel<I, true, wideRegenWaves(I), true>;
   return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
 }
 template <int I>
 static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, bool wide) {
   if (wide && cull)
-    hipLaunchKernelGGL((regenKernel<I, true, WIDE_REGEN_WAVES, true>), dim3(grid), dim3(BLOCK), 0, s, p);
+    hipLaunchKernelGGL((regenKernel<I, true, wideRegenWaves(I), true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else hipLaunchKernelGGL((regenKernel<I, false>), dim3(grid), dim3(BLOCK), 0, s, p);
   return hipGetLastError();
@@ -411,6 +417,6 @@ hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb) {
 }
 
 int regenLdsStack() { return REGEN_LDS_STACK; }
-int regenTop4() { return REGEN_TOP4; }
+int regenTop4(int integrator) { return regenTop4W(wideRegenWaves(integrator)); }
 
 }  // namespace pt

@@ -1753,7 +1753,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
                                    &noOrder);
   // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
   if (regen && wide && ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE)) useFast = true;
-  if (regen && wide) p.scene.f4nTop = std::min(regenTop4(), ctx->f4nDev);  // its own LDS copy's size
+  if (regen && wide) p.scene.f4nTop = std::min(regenTop4(c.integrator), ctx->f4nDev);  // its own LDS copy's size
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
