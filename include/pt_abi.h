@@ -238,7 +238,9 @@ int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked);
  * tiles (pt_display_own) and the other ranks' (pt_display_unpack: dpacked[k] = rank k's
  * packed buffer for k = 1..world-1, world <= 16, one launch) into one width x height
  * RGBA8 device image. With tile_world 1, pt_display_own writes every pixel. All on the
- * context's current stream, after the frames rendered so far; device pointers. */
+ * context's current stream, after the frames rendered so far; device pointers (work
+ * another stream queued on those buffers is not ordered before it: set that stream
+ * with pt_set_stream, or synchronise it first). */
 int pt_display_pack(pt_ctx* ctx, float limit, float gamma, void* dpacked);
 int pt_display_own(pt_ctx* ctx, float limit, float gamma, void* dimage);
 int pt_display_unpack(pt_ctx* ctx, int world, const void* const* dpacked, void* dimage);

@@ -35,6 +35,7 @@ def _render_full(cfg, tris, nodes, hdr, eye, rot):
         for f in range(FRAMES):
             r.render_frame(eye, rot, f)
         img = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()  # the fill (torch's stream) before the renderer's stream writes it
         r.display_own(img.data_ptr())
         r.synchronize()
         return r.accum(), r.stats().rays, img.cpu().numpy()

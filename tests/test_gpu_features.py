@@ -190,6 +190,7 @@ def test_display_frame_is_pass3_in_an_8bit_window(gamma):
             r.render_frame(eye, rot, f)
         t = r.tonemap(1.5, gamma)
         img = torch.zeros((180, 320, 4), dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()  # the fill (torch's stream) before the renderer's stream writes it
         r.display_own(img.data_ptr(), 1.5, gamma)
         r.synchronize()
     got = img.cpu().numpy()
@@ -205,6 +206,7 @@ def test_display_split_reassembles_the_frame():
     eye, rot = orbit_camera(*cfg.camera)
     W, H, world = 200, 130, 3
     full = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()  # torch's fills before the renderers' streams write these buffers
     with Renderer(W, H, "lambert") as r:
         r.upload_scene(tris, nodes)
         r.upload_env(hdr)
@@ -219,10 +221,12 @@ def test_display_split_reassembles_the_frame():
             rr.upload_env(hdr)
             rr.render_frame(eye, rot, 0)
             buf = torch.zeros(rr.owned_pixel_count() * 3, dtype=torch.uint8, device="cuda:0")
+            torch.cuda.synchronize()
             rr.display_pack(buf.data_ptr())
             rr.synchronize()
             packed.append(buf)
         img = torch.full((H, W, 4), 7, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
         rs[0].display_own(img.data_ptr())
         rs[0].synchronize()
         own_only = img.cpu().numpy()

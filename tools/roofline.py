@@ -22,7 +22,7 @@ the PSNR check's basicKernel are other kernels).
 Derived per-launch work (MI355X_MICROARCH.md):
   valu_insts = SQ_INSTS_VALU (wave64 instructions; peak issue 1024 SIMDs x 2.4 GHz / 2 cycles)
   dram_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   (KiB units; gfx950 FETCH_SIZE halving)
-  l2_hit     = TCC_HIT / (TCC_HIT + TCC_MISS);  clock_ghz = GRBM_GUI_ACTIVE / 8 / kernel time
+  l2_hit     = TCC_HIT / (TCC_HIT + TCC_MISS);  clock_ghz = GRBM_GUI_ACTIVE / 8 / dispatch time, per sq-pass dispatch
 """
 import csv
 import glob
@@ -100,7 +100,13 @@ def main():
                     rows_out.append({"pass": name, **r})
                 r0 = by_disp[di][0]
                 if name == "sq" and r0.get("End_Timestamp"):  # the counter pass's own dispatch duration
-                    vals["_counter_dispatch_ms"].append((int(r0["End_Timestamp"]) - int(r0["Start_Timestamp"])) / 1e6)
+                    dms = (int(r0["End_Timestamp"]) - int(r0["Start_Timestamp"])) / 1e6
+                    vals["_counter_dispatch_ms"].append(dms)
+                    # the clock of this dispatch: its own GRBM_GUI_ACTIVE (8 XCDs) over its own duration
+                    # (GRBM_GUI_ACTIVE is also sampled in the mem pass, whose dispatches last differently)
+                    gg = [float(r["Counter_Value"]) for r in by_disp[di] if r["Counter_Name"] == "GRBM_GUI_ACTIVE"]
+                    if gg and dms > 0:
+                        vals["_clock_ghz"].append(gg[0] / 8 / (dms * 1e-3) / 1e9)
         with open(d / "counters.csv", "w", newline="") as fh:
             wr = csv.DictWriter(fh, fieldnames=["pass"] + header)
             wr.writeheader()
@@ -109,6 +115,8 @@ def main():
         g = lambda k: m.get(k, float("nan"))  # noqa: E731
         cms = m.pop("_counter_dispatch_ms", float("nan"))
         vals.pop("_counter_dispatch_ms", None)
+        clock = m.pop("_clock_ghz", float("nan"))
+        vals.pop("_clock_ghz", None)
         # the kernel with nothing overlapping it: the serial-frames trace (PT_FLAG_SERIAL_FRAMES)
         serial_ms = None
         sp = sorted(glob.glob(f"{prof}/serial/**/run_kernel_trace.csv", recursive=True))
@@ -124,10 +132,10 @@ def main():
             "dram_bytes": round((2 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024),
             "l2_hit": round(g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")), 4),
             "valu_lane_util": round(g("SQ_THREAD_CYCLES_VALU") / (64 * g("SQ_ACTIVE_INST_VALU")), 4),
-            # GRBM_GUI_ACTIVE summed over the 8 XCDs, over the counter pass's own (serialised)
-            # dispatch durations -- the interval the counters describe
+            # per dispatch of the sq pass: GRBM_GUI_ACTIVE summed over the 8 XCDs over that dispatch's
+            # own (serialised) duration -- the interval its counters describe -- averaged
             "counter_dispatch_ms": round(cms, 4),
-            "clock_ghz_profiled": round(g("GRBM_GUI_ACTIVE") / 8 / (cms * 1e-3) / 1e9, 3),
+            "clock_ghz_profiled": round(clock, 3),
             "serial_kernel_ms": serial_ms,
             "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())},
             "samples": {k: len(v) for k, v in sorted(vals.items())},
