@@ -116,7 +116,13 @@ constexpr int PKT_DEPTH = 128;    // camera-ray packet stack entries per wave (L
 constexpr int PAIR_F4 = 7;        // float4 per pair record (26 floats: p1, p2, p3, Ng, w of two triangles)
 constexpr int HIT_F4 = 4;         // float4 per hit record (SceneView::hitRec)
 constexpr int MAT_F4 = 5;         // float4 per material (SceneView::mats)
-constexpr int W4_F4 = 8;          // float4 per 4-wide node (SceneView::fbvh4), one 128-byte line
+constexpr int W4_F4 = 8;          // float4 per 4-wide node as built (collapseWide4Device, encodeWide4), one 128-byte line
+// PT_W4_HALF: the traversals' 4-wide records hold the child boxes as halves rounded outward
+// (lo down, hi up; 48 bytes) + the refs: 64 bytes per visit instead of 112 (halfNodes4)
+#ifndef PT_W4_HALF
+#define PT_W4_HALF 0
+#endif
+constexpr int W4_NODE_F4 = PT_W4_HALF ? 4 : W4_F4;  // float4 per record of SceneView::fbvh4
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;
 constexpr int MAX_LEAF = 1 << LEAF_CNT_BITS;
@@ -367,6 +373,8 @@ hipError_t launchDisplayOwn(const PackParams& p, const float4* accum, float limi
                             hipStream_t s);
 hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image, hipStream_t s);
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s);
+// PT_W4_HALF: the built 4-wide records (W4_F4 float4 each) as traversal records (W4_NODE_F4)
+hipError_t launchHalfNodes4(const float4* full, int n, float4* half, hipStream_t s);
 // the running-mean update of a pipelined frame over the rank's owned pixels (PackParams
 // mapping): accum = mix(accum, col, 1 / (frameCounter + 1)) (IS:868-871, pass2.fsh:15)
 hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s);

@@ -18,6 +18,7 @@
 //    instead of the reference's three); triangles as 64-byte records with the
 //    precomputed unit normal and plane offset.
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 
 #include <cstdlib>
 #include <stdint.h>
@@ -957,7 +958,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     const bool w4 = PT_WIDE4 == 2 && !COUNT && p.scene.fast;  // the 4-wide tree's top
     const float4* src = w4 ? p.scene.fbvh4 : p.scene.fast ? p.scene.fbvh : p.scene.bvh;  // the tree traversed first
     // the copy's size from the staged tree's own record kind (never the other tree's: DESIGN.md §8)
-    const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.fast ? p.scene.fnTop * nodeF4<FAST_KIND>() : p.scene.nTop * 4;
+    const int n = w4 ? p.scene.f4nTop * W4_NODE_F4 : p.scene.fast ? p.scene.fnTop * nodeF4<FAST_KIND>() : p.scene.nTop * 4;
     for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
   }
   __syncthreads();
@@ -1359,6 +1360,31 @@ hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image,
   if (world < 2 || most <= 0) return hipSuccess;
   hipLaunchKernelGGL(displayUnpackKernel, dim3((unsigned)((most + 255) / 256), (unsigned)(world - 1)), dim3(256), 0, s,
                      d, image);
+  return hipGetLastError();
+}
+__global__ void halfNodes4Kernel(const float4* full, int n, float4* half) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4* r = full + (size_t)i * W4_F4;
+  auto pk = [](float x, float y, bool up) {  // two planes as halves, rounded outward
+    const __half a = up ? __float2half_ru(x) : __float2half_rd(x), b = up ? __float2half_ru(y) : __float2half_rd(y);
+    return __uint_as_float((uint32_t)__half_as_ushort(a) | (uint32_t)__half_as_ushort(b) << 16);
+  };
+  float w[12];
+  for (int a = 0; a < 6; a++) {  // lo.x, lo.y, lo.z, hi.x, hi.y, hi.z
+    const float4 v = r[a];
+    w[2 * a] = pk(v.x, v.y, a >= 3);
+    w[2 * a + 1] = pk(v.z, v.w, a >= 3);
+  }
+  float4* o = half + (size_t)i * 4;
+  o[0] = make_float4(w[0], w[1], w[2], w[3]);
+  o[1] = make_float4(w[4], w[5], w[6], w[7]);
+  o[2] = make_float4(w[8], w[9], w[10], w[11]);
+  o[3] = r[6];
+}
+hipError_t launchHalfNodes4(const float4* full, int n, float4* half, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(halfNodes4Kernel, dim3((n + 255) / 256), dim3(256), 0, s, full, n, half);
   return hipGetLastError();
 }
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s) {

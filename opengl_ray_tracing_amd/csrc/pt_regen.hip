@@ -256,12 +256,12 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   // the top of the uploaded tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
   constexpr int TOP4 = regenTop4W(WAVES);
-  constexpr int TOPF4 = (W4 && TOP4 * W4_F4 > LDS_NODES * 4) ? TOP4 * W4_F4 : LDS_NODES * 4;
+  constexpr int TOPF4 = (W4 && TOP4 * W4_NODE_F4 > LDS_NODES * 4) ? TOP4 * W4_NODE_F4 : LDS_NODES * 4;
   __shared__ float4 s_nodes[TOPF4];
   {
     const bool w4 = W4 && p.scene.fast;
     const float4* src = w4 ? p.scene.fbvh4 : p.scene.bvh;
-    const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.nTop * 4;  // the staged tree's own record size
+    const int n = w4 ? p.scene.f4nTop * W4_NODE_F4 : p.scene.nTop * 4;  // the staged tree's own record size
     for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
   }
   __syncthreads();

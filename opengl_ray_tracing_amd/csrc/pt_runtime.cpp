@@ -1026,6 +1026,14 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
     encodeWide4(an.data(), nn, h.nTri, 1e-5f, 3e-5f * scale, w4, ctx->f4Root, ctx->f4nDev, ctx->f4Depth);
     if ((rc = upload(ctx, &ctx->d_fbvh4, w4))) return rc;
   }
+  if (PT_W4_HALF) {  // the traversals' records: child planes as halves rounded outward (halfNodes4Kernel)
+    float4* hn = nullptr;
+    CK(hipMalloc(&hn, (size_t)std::max(ctx->f4nDev, 1) * W4_NODE_F4 * sizeof(float4)));
+    CK(launchHalfNodes4(ctx->d_fbvh4, ctx->f4nDev, hn, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    dfree(ctx->d_fbvh4);
+    ctx->d_fbvh4 = hn;
+  }
   ctx->fast4Ready = true;
   // a visit pushes up to three children: the traversal stack needs 3 entries per wide level
   ctx->maxStack = std::max(ctx->maxStack, 3 * ctx->f4Depth + 2);
@@ -1328,7 +1336,7 @@ static SceneView sceneView(const pt_ctx* ctx) {
   s.fnTop = std::min(LDS_NODES, ctx->fnDev);
   s.fbvh4 = ctx->d_fbvh4;
   s.f4Root = ctx->f4Root;
-  s.f4nTop = std::min(LDS_NODES * 4 / W4_F4, ctx->f4nDev);  // the LDS copy holds LDS_NODES * 4 float4
+  s.f4nTop = std::min(LDS_NODES * 4 / W4_NODE_F4, ctx->f4nDev);  // the LDS copy holds LDS_NODES * 4 float4
   s.refLeafOf = ctx->d_refLeafOf;
   s.refParent = ctx->d_refParent;
   s.refBox = ctx->d_refBox;

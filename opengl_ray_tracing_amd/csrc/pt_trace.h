@@ -401,6 +401,31 @@ __device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
   ka = k;
   ra = r;
 }
+// one 4-wide record: child planes lo/hi per axis (children 0..3 in x..w) and the refs
+__device__ __forceinline__ float2 halves2(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return make_float2((float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu)),
+                     (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)));
+}
+__device__ __forceinline__ float4 halves4(float a, float b) {
+  const float2 p = halves2(a), q = halves2(b);
+  return make_float4(p.x, p.y, q.x, q.y);
+}
+__device__ __forceinline__ void loadNode4(const float4* nd, float4& lx, float4& ly, float4& lz, float4& hx, float4& hy,
+                                          float4& hz, float4& rf) {
+#if PT_W4_HALF
+  const float4 a = nd[0], b = nd[1], c = nd[2];
+  rf = nd[3];
+  lx = halves4(a.x, a.y);
+  ly = halves4(a.z, a.w);
+  lz = halves4(b.x, b.y);
+  hx = halves4(b.z, b.w);
+  hy = halves4(c.x, c.y);
+  hz = halves4(c.z, c.w);
+#else
+  lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+#endif
+}
 template <bool CULL, class StackType, bool LDSTOP>
 __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
                                          bool anyRT, const float4* top, bool* tie) {
@@ -420,9 +445,10 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
         C.nodes++;
         if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
       }
-      const float4* nd = S.fbvh4 + (size_t)W4_F4 * ref;
-      if (LDSTOP && ref < S.f4nTop) nd = top + W4_F4 * ref;
-      const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+      const float4* nd = S.fbvh4 + (size_t)W4_NODE_F4 * ref;
+      if (LDSTOP && ref < S.f4nTop) nd = top + W4_NODE_F4 * ref;
+      float4 lx, ly, lz, hx, hy, hz, rf;
+      loadNode4(nd, lx, ly, lz, hx, hy, hz, rf);
       float key[4];
       int r[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
       const float lim = tbest + 1e-3f * fmaxf(1.0f, tbest);
@@ -547,9 +573,10 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
     if (__ballot(!done) == 0 || __popcll(__ballot(done)) >= yield) break;  // wave-uniform
     if (done) continue;
     while (w.ref >= 0) {
-      const float4* nd = S.fbvh4 + (size_t)W4_F4 * w.ref;
-      if (LDSTOP && w.ref < S.f4nTop) nd = top + W4_F4 * w.ref;
-      const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+      const float4* nd = S.fbvh4 + (size_t)W4_NODE_F4 * w.ref;
+      if (LDSTOP && w.ref < S.f4nTop) nd = top + W4_NODE_F4 * w.ref;
+      float4 lx, ly, lz, hx, hy, hz, rf;
+      loadNode4(nd, lx, ly, lz, hx, hy, hz, rf);
       float key[4];
       int r[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
       const float lim = w.tbest + 1e-3f * fmaxf(1.0f, w.tbest);
