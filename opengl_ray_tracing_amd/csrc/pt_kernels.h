@@ -118,7 +118,10 @@ constexpr int HIT_F4 = 4;         // float4 per hit record (SceneView::hitRec)
 constexpr int MAT_F4 = 5;         // float4 per material (SceneView::mats)
 constexpr int W4_F4 = 8;          // float4 per 4-wide node as built (collapseWide4Device, encodeWide4), one 128-byte line
 // PT_W4_HALF: the traversals' 4-wide records hold the child boxes as halves rounded outward
-// (lo down, hi up; 48 bytes) + the refs: 64 bytes per visit instead of 112 (halfNodes4)
+// (lo down, hi up; 48 bytes) + the refs: 64 bytes per visit instead of 112 (halfNodes4).
+// Bit-exact (tools/variant_digest.py c2, c4) but slower: c2 0.2346 -> 0.2387 ms, c4 0.3232 ->
+// 0.3236, c5 5.75 -> 5.93 (the 24 conversions per visit and the looser boxes cost more than
+// the texture-path bytes saved), so off
 #ifndef PT_W4_HALF
 #define PT_W4_HALF 0
 #endif
