@@ -371,6 +371,11 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
     const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
     ctx->pipeDepth = std::min(ctx->pipeDepth, std::max(2, hwq - 2));
+    // Whole Lambert frames (the regen kernel on every scene): 6 in flight. c2's bench line (20 frames
+    // from an idle GPU) 0.254-0.257 ms per frame at 6 vs 0.259-0.277 at 8 and 0.259 at 4, 100 frames
+    // 0.232 either way; the MIS megakernel keeps 8 (c4 0.366 at 8 vs 0.373-0.397 at 6, 0.41 at 4),
+    // and so do screen-tile shares (c2's 1/8 share 0.061 at 8 vs 0.074 at 6)
+    if (cfg->integrator == 0 && ctx->regenWide != 0 && cfg->tile_world <= 1) ctx->pipeDepth = std::min(ctx->pipeDepth, 6);
     if (const char* e = std::getenv("PT_PIPE_DEPTH")) ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
