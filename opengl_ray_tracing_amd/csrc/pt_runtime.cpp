@@ -153,6 +153,9 @@ struct pt_ctx {
   // frame streams at the lowest stream priority (PT_SLOT_PRIORITY=1; measured slower: an N = 8 share
   // of c2 0.065 -> 0.105 ms per frame)
   bool slotPriority = false;
+  // PT_GRID_ALWAYS=1: a frame's grid is its share even with no other frame in flight (bench line, 20
+  // frames from idle: c2 0.2532 / 0.2532 -> 0.2476 / 0.2578 ms, c4 0.373 / 0.368 -> 0.370 / 0.365: noise)
+  bool gridAlways = false;
   // the running mean updated tile by tile inside the frame kernels (renderKernel completeItem;
   // PT_KERNEL_MIX=1; off: mixKernel per frame on the caller's stream): per colour buffer and tile
   // the pixels written, per tile the lock word (2 x next frame to mix); valid from frame
@@ -380,6 +383,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
     if (const char* e = std::getenv("PT_SLOT_PRIORITY")) ctx->slotPriority = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PT_GRID_ALWAYS")) ctx->gridAlways = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_KERNEL_MIX")) ctx->kernelMix = std::atoi(e) != 0;
     CKC(hipEventCreateWithFlags(&ctx->protoInit, hipEventDisableTiming));
     CKC(hipEventCreateWithFlags(&ctx->callerMark, hipEventDisableTiming));
@@ -1693,7 +1697,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const int fullGrid = ctx->numCU * nb;
   int grid = fullGrid;
   if (piped && D > 1 && ctx->gridShare) {
-    bool others = false;  // another frame still in flight: the caller streams frames
+    bool others = ctx->gridAlways;  // another frame still in flight: the caller streams frames
     for (int k = 0; k < D && !others; k++)
       others = k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
     (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
