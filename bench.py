@@ -103,9 +103,6 @@ def main():
         _native.use_variant(os.environ["PT_VARIANT"])
     from opengl_ray_tracing_amd import FLAG_COUNT_FETCHES, Renderer, orbit_camera, scenes
 
-    cfg, tris, nodes, hdr = scenes.build_config(args.config, args.builder)
-    eye, rot = orbit_camera(*cfg.camera)
-
     torch = None
     if n > 1:
         import torch
@@ -114,6 +111,18 @@ def main():
             local = 0
         torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend, init_method="env://")
+        # the scene is prepared once, on rank 0, and broadcast: N ranks building c5's
+        # 1M-triangle tree at once would only contend for the host's cores
+        from opengl_ray_tracing_amd.distributed import broadcast_scene
+        cfg = scenes.CONFIGS[args.config]
+        if cfg.integrator == "basic":  # the BASIC shapes are 19 records of doubles: built locally
+            cfg, tris, nodes, hdr = scenes.build_config(args.config, args.builder)
+        else:
+            tris, nodes, hdr = broadcast_scene(lambda: scenes.build_config(args.config, args.builder)[1:], rank,
+                                               None if args.dist_backend == "gloo" else f"cuda:{local}")
+    else:
+        cfg, tris, nodes, hdr = scenes.build_config(args.config, args.builder)
+    eye, rot = orbit_camera(*cfg.camera)
 
     tiles = n > 1 and args.shard == "tiles"
     split = dict(tile_rank=rank, tile_world=n) if tiles else dict(sample_rank=rank, sample_world=n)
