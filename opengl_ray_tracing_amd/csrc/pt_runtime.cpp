@@ -143,6 +143,8 @@ struct pt_ctx {
   // frames in flight (PIPE slots; see PIPE above)
   bool pipe = false;                        // this context pipelines its megakernel frames
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
+  int pipeDepthBase = PT_PIPE;              // ... as chosen at creation (uploadScene may lower it for large scenes)
+  bool pipeDepthFixed = false;              // PT_PIPE_DEPTH set: no scene-dependent choice
   bool gridShare = true;                    // frames in flight split the persistent grid (PT_GRID_SHARE=0: not)
   // % of residency the frames in flight split (PT_GRID_PCT): 150 -- each frame's grid half again its
   // equal share, so a frame finishing early leaves waves of the others ready to take its place --
@@ -379,7 +381,11 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     // 0.232 either way; the MIS megakernel keeps 8 (c4 0.366 at 8 vs 0.373-0.397 at 6, 0.41 at 4),
     // and so do screen-tile shares (c2's 1/8 share 0.061 at 8 vs 0.074 at 6)
     if (cfg->integrator == 0 && ctx->regenWide != 0 && cfg->tile_world <= 1) ctx->pipeDepth = std::min(ctx->pipeDepth, 6);
-    if (const char* e = std::getenv("PT_PIPE_DEPTH")) ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("PT_PIPE_DEPTH")) {
+      ctx->pipeDepth = std::min(PIPE, std::max(1, std::atoi(e)));
+      ctx->pipeDepthFixed = true;
+    }
+    ctx->pipeDepthBase = ctx->pipeDepth;
     if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
     if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
     if (const char* e = std::getenv("PT_SLOT_PRIORITY")) ctx->slotPriority = std::atoi(e) != 0;
@@ -968,6 +974,15 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   ctx->nTri = h.nTri;
   ctx->nNodes = h.nNodes;
   ctx->nDevNodes = h.ref.nDev;
+  // Large Disney/MIS scenes (the regen kernel's, renderOne wideScene) run 4 frames in flight:
+  // c5's frames last ~6 ms, and 8 in flight spend more on the pipeline's fill and drain than
+  // they gain (bench line, 20 frames from idle: 5.60-5.66 ms per frame at 4 vs 5.88 at 8, 6.00 at 6)
+  if (ctx->pipe && !ctx->pipeDepthFixed) {
+    const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + HIT_F4 * 16) + (size_t)ctx->nDevNodes * 64;
+    const bool wideScene = ctx->cfg.integrator != 0 && !(ctx->cfg.flags & PT_FLAG_NO_CULL) &&
+                           sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
+    ctx->pipeDepth = wideScene ? std::min(ctx->pipeDepthBase, 4) : ctx->pipeDepthBase;
+  }
   ctx->rootRef = h.ref.rootRef;
   ctx->depth = h.ref.depth;
   ctx->maxStack = h.ref.depth + 1;
