@@ -8,10 +8,14 @@ OpenglRayTracing bunny scene (5k tris) at 1920x1080, Lambert, 2 bounces.
 
 N > 1 ranks (one process per GPU):
   --shard tiles (default, strong scaling: BASELINE north_star's split): every
-      rank renders its 32x32 screen tiles of the one frame; every step presents
-      the frame on rank 0 by an RCCL gather of the packed shards (bit-exact
-      reassembly), pipelined one frame deep: frame f's gather runs on a
-      communication stream while frame f+1 renders.
+      rank renders its 32x32 screen tiles of the one frame, in batches of
+      tile_world frames per launch (pt_render_frames_async: each frame 1 spp and
+      its own running-mean update, about one whole image's work per launch);
+      after every batch the running means of the rank's pixels (f32 radiance,
+      12 B/pixel) are gathered to rank 0 over RCCL (bit-exact reassembly),
+      pipelined one batch deep: batch b's gather runs on a communication stream
+      while batch b+1 renders. --gather display moves the displayed frame
+      (pass3 tonemap in the 8-bit window, 3 B/pixel) instead.
   --shard samples (weak scaling): every rank renders the whole frame from its
       own interleaved sample stream (rank r: samples r, r+N, ...), no
       collective per step; the ranks' running means are combined by one RCCL
@@ -76,9 +80,12 @@ def parse():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N > 1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="rehearsal: every rank on device 0")
-    ap.add_argument("--gather", choices=["display", "accum"], default="display",
-                    help="--shard tiles: per frame, gather the displayed frame (RGB8, 3 B/pixel; the running "
-                         "means gathered once after the run) or the running means (3 f32 per pixel)")
+    ap.add_argument("--gather", choices=["display", "accum"], default="accum",
+                    help="--shard tiles: after every batch of frames, gather the running means (f32 radiance, "
+                         "3 f32 per pixel) or the displayed frame (RGB8, 3 B/pixel; the running means then "
+                         "gathered once after the run)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per launch (pt_config.frame_batch; 0 = the renderer's choice: tile_world)")
     ap.add_argument("--shard", choices=["samples", "tiles"], default="tiles",
                     help="N > 1: sample-parallel full frames (weak) or screen-tile shards of one frame (strong)")
     return ap.parse_args()
@@ -127,7 +134,7 @@ def main():
     tiles = n > 1 and args.shard == "tiles"
     split = dict(tile_rank=rank, tile_world=n) if tiles else dict(sample_rank=rank, sample_world=n)
     r = Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=local,
-                 flags=args.flags, **split)
+                 flags=args.flags, frame_batch=args.batch, **split)
     r.upload_scene(tris, nodes)
     r.upload_env(hdr)
 
@@ -152,11 +159,19 @@ def main():
         from opengl_ray_tracing_amd.distributed import SampleReduce
         combine = SampleReduce(r, rank, n, f"cuda:{local}")
 
-    def step(frame, cam=None):
+    batch = r.stats().frame_batch  # frames per launch (the renderer's; 1 at N = 1)
+
+    def frames(first, n, cam=None):
+        """frames first .. first+n-1: batches of `batch` frames (one launch each, every frame its own
+        1 spp and running-mean update), each followed by the gather to rank 0 when N > 1"""
         e, c = cam if cam is not None else (eye, rot)
-        r.render_frame(e, c, frame, sync=False)
-        if gather is not None:
-            gather()
+        k = 0
+        while k < n:
+            m = min(batch, n - k)
+            r.render_frames(e, c, first + k, m)
+            if gather is not None:
+                gather()
+            k += m
 
     def sync_all():
         r.synchronize()
@@ -169,15 +184,12 @@ def main():
     # first 13 frames after a running-mean restart (pt_runtime.cpp probePolicy); those
     # frames run before the W warmup steps, so the timed frames are the
     # progressive steady state (same image, bit for bit, either way).
-    for f in range(PROBE_FRAMES):
-        step(f)
-    for f in range(args.warmup):
-        step(PROBE_FRAMES + f)
+    frames(0, PROBE_FRAMES)
+    frames(PROBE_FRAMES, args.warmup)
     sync_all()
     r.reset_stats()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(PROBE_FRAMES + args.warmup + k)
+    frames(PROBE_FRAMES + args.warmup, args.steps)
     sync_all()
     t1 = time.perf_counter()
     st = r.stats()
@@ -190,8 +202,7 @@ def main():
     if not args.no_reset:
         moved = orbit_camera(cfg.camera[0] + 1.0, *cfg.camera[1:])
         t2 = time.perf_counter()
-        for f in range(PROBE_FRAMES):
-            step(f, moved)
+        frames(0, PROBE_FRAMES, moved)
         sync_all()
         reset_ms = 1e3 * (time.perf_counter() - t2) / PROBE_FRAMES
     # the frame kernel's own duration with nothing overlapping it: the same workload with frames
@@ -247,19 +258,19 @@ def main():
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
         mrays = rays_total / elapsed / 1e6
-        rays_per_launch = rays_local / max(st.launches, 1)
+        rays_per_frame = rays_local / max(st.frames, 1)
         # frames in flight overlap their kernels, so a launch's own duration overstates its share of
         # the device: the roofline then divides by the wall time per frame (frame kernel + reorder +
         # running-mean update) instead
         pipelined = st.frames_in_flight > 1
-        roofline = make_roofline(args, cfg, ms_per_step if pipelined else kernel_ms_avg, rays_per_launch,
+        roofline = make_roofline(args, cfg, ms_per_step if pipelined else kernel_ms_avg, rays_per_frame,
                                  bytes_per_ray, n)
         roofline["time_basis"] = ("wall ms per frame (frames in flight)" if pipelined
                                   else "frame kernel HIP-event ms")
         roofline["launch_ms"] = round(kernel_ms_avg, 4)
         roofline["kernel"] = ("regenKernel<%s>" if st.regen else "renderKernel<%s>") % cfg.integrator
         if serial_ms is not None:
-            kb = make_roofline(args, cfg, serial_ms, rays_per_launch, bytes_per_ray, n)
+            kb = make_roofline(args, cfg, serial_ms, rays_per_frame, bytes_per_ray, n)
             roofline["kernel_basis"] = {
                 "time_basis": "frame kernel HIP-event ms, frames issued serially (PT_FLAG_SERIAL_FRAMES)",
                 "kernel_ms": round(serial_ms, 4), "frames": SERIAL_FRAMES, "bound": kb["bound"],
@@ -284,9 +295,11 @@ def main():
                        "traversal_tree": "runtime (checked against uploaded)" if st.runtime_tree else "uploaded",
                        "frame_kernel": "path regeneration" if st.regen else "lock-step megakernel",
                        "waves_per_simd": st.waves_per_simd, "frames_in_flight": st.frames_in_flight,
-                       "parallelism": (f"screen-tile x{n}" + ((" + RCCL gather per frame of the displayed frame "
-                                                               "(RGB8)" if args.gather == "display" else
-                                                               " + RCCL gather per frame of the running means (f32)")
+                       "frames_per_launch": batch,
+                       "parallelism": (f"screen-tile x{n}" + ((f" + RCCL gather of the displayed frame (RGB8) per "
+                                                               f"batch of {batch} frames" if args.gather == "display"
+                                                               else f" + RCCL gather of the running means (f32 "
+                                                               f"radiance) per batch of {batch} frames")
                                                               if n > 1 else ""))
                        if args.shard == "tiles" else
                        (f"sample-parallel x{n}" + (" (RCCL reduce of the running means after the run)"
@@ -301,7 +314,7 @@ def main():
         dist.destroy_process_group()
 
 
-def make_roofline(args, cfg, kernel_ms, rays_per_launch, bytes_per_ray, n):
+def make_roofline(args, cfg, kernel_ms, rays_per_frame, bytes_per_ray, n):
     """Roofline of the frame kernel. Each resource's per-launch work comes from the hardware
     counters of the same workload (profiles/r3/counters.json, tools/roofline.py, one rocprofv3
     pass per counter group over this bench's timed frames); divided by this run's live kernel
@@ -313,10 +326,10 @@ def make_roofline(args, cfg, kernel_ms, rays_per_launch, bytes_per_ray, n):
     counted by the instrumented kernel) over the same time -- what pass1.fsh would have to
     move, not what this kernel moves (its tree, culling and packets fetch far less)."""
     t = kernel_ms * 1e-3
-    eq = rays_per_launch * bytes_per_ray / t / 1e9
+    eq = rays_per_frame * bytes_per_ray / t / 1e9
     base = {"kernel": "renderKernel<%s>" % cfg.integrator, "kernel_ms": round(kernel_ms, 4),
             "equivalent_GBs": round(eq, 1), "bytes_per_ray": round(bytes_per_ray, 1),
-            "rays_per_launch": int(rays_per_launch)}
+            "rays_per_frame": int(rays_per_frame)}
     ent = None
     p = Path(args.counters) if args.counters else None
     if p and p.exists() and not args.flags and not args.builder and n == 1:

@@ -26,10 +26,12 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 5  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
+#define PT_ABI_VERSION 6  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
                              3: scene-upload fields at the end of pt_frame_stats, pt_build_bvh_device;
                              4: BASIC shapes as doubles, its double image, the replayed random stream;
-                             5: the displayed frame of a screen-tile split (pt_display_*) */
+                             5: the displayed frame of a screen-tile split (pt_display_*);
+                             6: batches of frames (pt_render_frames_async, pt_config.frame_batch,
+                                pt_frame_stats.frames), pt_config.hw_queues */
 
 /* error codes */
 #define PT_OK 0
@@ -97,6 +99,11 @@ typedef struct pt_config {
   int n_devices;
   int device_ids[PT_MAX_DEVICES];
   int gather;
+  /* ABI 6 */
+  int frame_batch;    /* pt_render_frames_async: most frames per launch (0 = automatic: tile_world
+                         frames of a screen-tile share, i.e. about one whole image's work per launch) */
+  int hw_queues;      /* hardware queues of the process's HIP runtime (GPU_MAX_HW_QUEUES in effect when
+                         HIP initialised; bounds the frames in flight); 0 = read GPU_MAX_HW_QUEUES now */
 } pt_config;
 
 /* Counters accumulate over every launch since pt_create / pt_reset_stats. */
@@ -128,6 +135,10 @@ typedef struct pt_frame_stats {
   int accel_depth;      /* and its depth (root = 1) */
   int regen;            /* 1: the last frame ran the path-regeneration kernel (PT_FLAG_REGEN, or a large
                            Disney/MIS scene), 0: the lock-step megakernel */
+  /* ABI 6 */
+  int64_t frames;       /* frames rendered by the launches since the reset (a batch launch renders
+                           several: pt_render_frames_async) */
+  int frame_batch;      /* most frames per launch of this context (pt_config.frame_batch, resolved) */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;
@@ -161,6 +172,11 @@ int pt_upload_shapes(pt_ctx* ctx, const double* shapes, int n);
  * summed by :427-429; row 0 = top), width x height x 3 f64 host buffer. The f32 accumulation
  * (pt_download_accum) holds the same sums rounded to float. */
 int pt_download_basic_image(pt_ctx* ctx, double* rgb);
+/* PT_BASIC_CPU_COMPAT checkpoint restore: the double image (as pt_download_basic_image wrote it);
+ * the next frame adds its sample to it, bit for bit as if the frames had not been interrupted.
+ * (pt_upload_accum on a BASIC context restores from the f32 sums: the double image is set to
+ * them, widened.) */
+int pt_upload_basic_image(pt_ctx* ctx, const double* rgb);
 
 /* PT_BASIC_CPU_COMPAT: replay a recorded random stream instead of the per-pixel counter RNG,
  * so a frame consumes exactly the random numbers the reference's serial run consumed
@@ -190,6 +206,15 @@ int pt_render_frame(pt_ctx* ctx, const float eye[3], const float cameraRotate[16
 /* Same without synchronising or downloading. */
 int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16],
                           uint32_t frameCounter);
+/* nFrames display() calls of one camera: frames frameCounter .. frameCounter + nFrames - 1, each
+ * 1 spp per owned pixel with its own running-mean update (bit for bit nFrames calls of
+ * pt_render_frame_async). Consecutive frames are rendered side by side in one launch (up to
+ * pt_config.frame_batch; while the tree / split policies are being measured, one each) and
+ * their running-mean updates applied together, pixel by pixel in frame order; the accumulation
+ * holds the last frame's mean when the call's work completes (a frame in between is not
+ * materialised in it). Without synchronising. */
+int pt_render_frames_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16],
+                           uint32_t frameCounter, int nFrames);
 
 /* The GPU binned-SAH builder (pt_build.hip), exposed as a scene
  * builder in the reference's node encoding -- the role of buildBVH / buildBVHwithSAH

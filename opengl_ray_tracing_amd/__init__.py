@@ -4,24 +4,32 @@ xfause/OpenGL_Ray_Tracing (include/pt_abi.h).
 Hot path: hand-written HIP kernels for gfx950 in csrc/, reached through the
 C ABI of libpt.so. There is no CPU fallback in this package.
 
-Frames in flight run on a HIP stream each: importing the package raises
-GPU_MAX_HW_QUEUES (hardware queues per process, HIP's default 4) to 12 unless
-PT_KEEP_HW_QUEUES is set; HIP reads it once, when it first initialises, so import this
-package before torch or anything else initialises HIP. The renderer sizes its pipeline
-to the queues the variable grants.
+Frames in flight run on a HIP stream each. HIP reads GPU_MAX_HW_QUEUES
+(hardware queues per process, its default 4) once, when it first initialises: importing this
+package sets it to 12 only when it is unset and HIP is not initialised yet (an explicit value is
+left alone), and records the value in effect (HW_QUEUES), which every Renderer passes to the
+runtime as pt_config.hw_queues -- the pipeline is sized to the queues the process really has.
 """
 import os
+import sys
 
 
-def _hw_queues(want: int = 12) -> None:
-    if os.environ.get("PT_KEEP_HW_QUEUES"):
-        return
+def _hip_initialised() -> bool:
+    torch = sys.modules.get("torch")
+    try:
+        return bool(torch is not None and torch.cuda.is_initialized())
+    except Exception:  # noqa: BLE001  (a partial torch import)
+        return False
+
+
+def _hw_queues(want: int = 12) -> int:
     cur = os.environ.get("GPU_MAX_HW_QUEUES", "")
-    if not cur.isdigit() or int(cur) < want:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
+    if not cur and not _hip_initialised():
+        os.environ["GPU_MAX_HW_QUEUES"] = cur = str(want)
+    return int(cur) if cur.isdigit() and int(cur) > 0 else 4
 
 
-_hw_queues()
+HW_QUEUES = _hw_queues()
 
 from .scene import (Material, Scene, calculate_hdr_cache, decode_hdr, get_transform_matrix, load_hdr,
                     orbit_camera, read_pfm, write_pfm, write_png)

@@ -13,7 +13,7 @@ from . import _build
 
 _lib = None
 
-ABI_VERSION = 5  # include/pt_abi.h PT_ABI_VERSION
+ABI_VERSION = 6  # include/pt_abi.h PT_ABI_VERSION
 c_float_p = C.POINTER(C.c_float)
 c_double_p = C.POINTER(C.c_double)
 c_int_p = C.POINTER(C.c_int)
@@ -26,6 +26,7 @@ class PtConfig(C.Structure):
         ("flags", C.c_uint32), ("basic_samples", C.c_int), ("basic_seed", C.c_uint32),
         ("sample_rank", C.c_int), ("sample_world", C.c_int),
         ("n_devices", C.c_int), ("device_ids", C.c_int * 8), ("gather", C.c_int),
+        ("frame_batch", C.c_int), ("hw_queues", C.c_int),
     ]
 
 
@@ -38,6 +39,7 @@ class PtFrameStats(C.Structure):
         ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int), ("frames_in_flight", C.c_int),
         ("upload_ms", C.c_float), ("accel_build_ms", C.c_float), ("accel_device", C.c_int),
         ("accel_nodes", C.c_int), ("accel_depth", C.c_int), ("regen", C.c_int),
+        ("frames", C.c_int64), ("frame_batch", C.c_int),
     ]
 
 
@@ -63,10 +65,12 @@ SIGNATURES = {
     "pt_upload_env": (C.c_int, [C.c_void_p, c_float_p, C.c_int, C.c_int, c_float_p]),
     "pt_upload_shapes": (C.c_int, [C.c_void_p, c_double_p, C.c_int]),
     "pt_download_basic_image": (C.c_int, [C.c_void_p, c_double_p]),
+    "pt_upload_basic_image": (C.c_int, [C.c_void_p, c_double_p]),
     "pt_set_basic_stream": (C.c_int, [C.c_void_p, c_double_p, C.c_int64, C.POINTER(C.c_int64), C.c_int64]),
     "pt_basic_replay_overruns": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
     "pt_render_frame": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32, c_float_p]),
     "pt_render_frame_async": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32]),
+    "pt_render_frames_async": (C.c_int, [C.c_void_p, c_float_p, c_float_p, C.c_uint32, C.c_int]),
     "pt_trace_closest": (C.c_int, [C.c_void_p, c_float_p, C.c_int, c_float_p, c_int_p]),
     "pt_build_bvh_device": (C.c_int, [C.c_void_p, c_float_p, C.c_int, C.c_int, c_float_p, C.c_int, c_int_p, c_int_p]),
     "pt_download_accum": (C.c_int, [C.c_void_p, c_float_p]),

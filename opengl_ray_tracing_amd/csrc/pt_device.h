@@ -162,26 +162,6 @@ __device__ __forceinline__ float2 ldStream(const float2* p) {
   return *p;
 #endif
 }
-// Cross-CU hand-off of 16-byte values inside one launch (MI355X_MICROARCH.md "Valid forms":
-// every store of the bytes sc1 (write-through), drained by s_waitcnt vmcnt(0) before the
-// signal; every load of them an sc1 global load): two relaxed agent-scope 8-byte atomics each.
-__device__ __forceinline__ void stCoherent(float4* p, float4 v) {
-  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-  __hip_atomic_store(q, (unsigned long long)__float_as_uint(v.x) | (unsigned long long)__float_as_uint(v.y) << 32,
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, (unsigned long long)__float_as_uint(v.z) | (unsigned long long)__float_as_uint(v.w) << 32,
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float4 ldCoherent(const float4* p) {
-  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
-  const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)), __uint_as_float((uint32_t)b),
-                     __uint_as_float((uint32_t)(b >> 32)));
-}
-// every vector memory access of this wave so far has completed (its sc1 stores are visible
-// device-wide): before a signal another CU acts on
-__device__ __forceinline__ void drainStores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void stStream(float4* p, float4 v) {
 #if PT_NT_STREAM
   const f32x4_t x = {v.x, v.y, v.z, v.w};

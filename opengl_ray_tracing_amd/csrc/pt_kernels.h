@@ -32,9 +32,6 @@ constexpr int WIDE_WAVES = 3;
 // (c5: 16 bounces) a lane that takes a new pixel when its path ends beats the
 // lock-step megakernel, whose waves last as long as their longest path (c5: 10.0
 // -> 9.2 ms; on the L2-resident c4 the regen kernel is 3.6x slower)
-#ifndef PT_REGEN_YIELD_REL
-#define PT_REGEN_YIELD_REL 0  // 1: PT_REGEN_YIELD counts 64ths of the lanes walking together, not lanes
-#endif
 #ifndef PT_WIDE_REGEN_WAVES
 #define PT_WIDE_REGEN_WAVES 4  // MIS
 #endif
@@ -83,25 +80,12 @@ constexpr size_t CTL_BYTES = CTL_RAYS + (size_t)RAY_SHARDS * 256;
 #ifndef PT_FAST_TREE
 #define PT_FAST_TREE 1  // build and traverse the runtime's own tree (results checked against the reference's)
 #endif
-#ifndef PT_QUANT_NODES
-#define PT_QUANT_NODES 0  // 1: the runtime tree's node records quantized to 8 bits per plane (measured slower: DESIGN.md)
-#endif
-constexpr bool FAST_QUANT = PT_QUANT_NODES != 0;
 #ifndef PT_WIDE4
 // the megakernel's traced rays walk the runtime tree collapsed to 4-wide nodes (pt_trace.h
 // traceRay4; camera rays keep their bins and the binary tree's packets): 2 = with the 4-wide
 // tree's top 64 nodes in LDS (c2 0.408 -> 0.376 ms, c4 0.498 -> 0.477, c3 0.273 -> 0.262),
 // 1 = without (c3 0.257, c2 0.380), 0 = the binary runtime tree
 #define PT_WIDE4 2
-#endif
-#ifndef PT_STATIC_PCT
-#define PT_STATIC_PCT 0  // megakernel in band order: % of the tiles dealt to the waves statically
-#endif
-#ifndef PT_CLAIM_AHEAD
-#define PT_CLAIM_AHEAD 0  // megakernel: claim the next tile when a tile starts (TileCursor::claimAhead)
-#endif
-#ifndef PT_LIGHT_PREFETCH
-#define PT_LIGHT_PREFETCH 0  // MIS: fetch the next bounce's env light sample before this bounce's walks
 #endif
 #ifndef PT_FUSED_SLABS
 #define PT_FUSED_SLABS 1  // the runtime tree's slab tests as packed FMAs (pt_trace.h visitNodeF)
@@ -117,15 +101,6 @@ constexpr int PAIR_F4 = 7;        // float4 per pair record (26 floats: p1, p2, 
 constexpr int HIT_F4 = 4;         // float4 per hit record (SceneView::hitRec)
 constexpr int MAT_F4 = 5;         // float4 per material (SceneView::mats)
 constexpr int W4_F4 = 8;          // float4 per 4-wide node as built (collapseWide4Device, encodeWide4), one 128-byte line
-// PT_W4_HALF: the traversals' 4-wide records hold the child boxes as halves rounded outward
-// (lo down, hi up; 48 bytes) + the refs: 64 bytes per visit instead of 112 (halfNodes4).
-// Bit-exact (tools/variant_digest.py c2, c4) but slower: c2 0.2346 -> 0.2387 ms, c4 0.3232 ->
-// 0.3236, c5 5.75 -> 5.93 (the 24 conversions per visit and the looser boxes cost more than
-// the texture-path bytes saved), so off
-#ifndef PT_W4_HALF
-#define PT_W4_HALF 0
-#endif
-constexpr int W4_NODE_F4 = PT_W4_HALF ? 4 : W4_F4;  // float4 per record of SceneView::fbvh4
 constexpr int LEAF_CNT_BITS = 5;  // leaf refs: ~(start << 5 | (count - 1)), count <= 32
 constexpr int REF_NONE = (int)0x80000000;
 constexpr int MAX_LEAF = 1 << LEAF_CNT_BITS;
@@ -176,13 +151,11 @@ struct Env {
   int w, h, res;        // res = hdrResolution
 };
 
-// A pipelined megakernel frame's colour buffer and running-mean weight, published in its slot
-// (frameVarKernel, before the frame's kernel) for the waves of earlier frames' kernels that
-// mix its tiles into the accumulation (renderKernel completeItem).
-struct FrameVar {
+// One frame of a launch as a work item sees it: its sample index (RNG seeds, Sobol
+// index) and its colour buffer (null: the running mean is updated in place).
+struct FrameRef {
   float4* col;
   uint32_t sampleIndex;
-  uint32_t frameCounter;  // the frame's running-mean weight is 1/(frameCounter+1)
 };
 
 struct RenderParams {
@@ -199,6 +172,14 @@ struct RenderParams {
   // sample colour here (float4, w unused) and leave the running mean to mixKernel, which
   // runs in frame order; null = mix into accum in place (IS:868-871)
   float4* col;
+  // A batch of nFrames consecutive frames of one camera in this launch (pt_render_frames_async):
+  // frame f draws sample index sampleIndex + f * sampleStride and writes its colours to
+  // col + f * colStride (pixels) and its camera-ray results to primHit + f * colStride. Work
+  // item k of the launch is item k / nFrames of frame k % nFrames, so the frames of one tile
+  // run side by side (the same camera rays, the same nodes). nFrames 1: a single frame.
+  int nFrames;
+  uint32_t sampleStride;
+  size_t colStride;
   // camera-ray bins (pt_primary.hip): per 8x8 tile of the whole image, binStart[t] ..
   // binStart[t+1] index binTris; null = every camera ray walks the BVH
   const int* binStart;
@@ -211,12 +192,8 @@ struct RenderParams {
   // packet); null = the megakernel traces its camera rays itself
   int2* primHit;
   int zeroQueue;  // the camera-ray pass zeroes `queue` for the frame kernel after it (no memset)
-  // band order (tileOrder null): items [0, staticItems) are dealt without atomics, wave w of
-  // the grid taking w, w + waves, ...; the rest, staticItems + q * dynPerQueue + i, are
-  // claimed from queue q as usual (staticItems 0: every item claimed)
-  int staticItems, dynPerQueue;
   int* queue;           // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
-  int perQueue;         // items per queue
+  int perQueue;         // items per queue (band), claimed once per frame of the launch
   int numItems;         // 8x8 wave tiles owned by this rank
   int shardSize;        // shard tile edge (multiple of 8)
   int shardTiles;       // (shardSize/8)^2
@@ -233,16 +210,6 @@ struct RenderParams {
   int* tileCost;        // per tile: summed cost of its items this frame (shader cycles), null = not recorded
   int* tileCostMax;     // per tile: its longest item this frame
   unsigned long long* waveTrace;  // PT_WAVE_TRACE builds only: 6 u64 per wave (pt_runtime.cpp, tools/wave_trace.py)
-  // frames in flight: this frame's sequence number, the slots, every slot's FrameVar
-  uint32_t seq;
-  int depth;
-  FrameVar* frameVars;
-  // The running mean updated inside the frame kernels (renderKernel completeItem), tile by tile in
-  // frame order: tileDone[(seq % (depth + 1)) * numItems + tile] counts the tile's pixels whose
-  // sample colour frame seq has written; mixState[tile] = 2 * (the next frame to mix into the
-  // tile) + 1 while a wave mixes it. null = mixKernel updates the running mean per frame.
-  int* tileDone;
-  unsigned* mixState;
 };
 
 struct TraceParams {
@@ -365,6 +332,9 @@ int regenLdsStack();
 int regenTop4(int integrator);  // 4-wide nodes the wide regen kernel stages in LDS (PT_REGEN_TOP4[_3])
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);
+// BASIC checkpoints: the double image from the f32 sums (widened), or the f32 sums from the double image
+hipError_t launchBasicWiden(const float4* accum, double* image, long n, hipStream_t s);
+hipError_t launchBasicNarrow(const double* image, float4* accum, long n, hipStream_t s);
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s);
 // PACK_F floats (r, g, b) per packed slot
 constexpr int PACK_F = 3;
@@ -376,12 +346,10 @@ hipError_t launchDisplayOwn(const PackParams& p, const float4* accum, float limi
                             hipStream_t s);
 hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image, hipStream_t s);
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s);
-// PT_W4_HALF: the built 4-wide records (W4_F4 float4 each) as traversal records (W4_NODE_F4)
-hipError_t launchHalfNodes4(const float4* full, int n, float4* half, hipStream_t s);
-// the running-mean update of a pipelined frame over the rank's owned pixels (PackParams
-// mapping): accum = mix(accum, col, 1 / (frameCounter + 1)) (IS:868-871, pass2.fsh:15)
-hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s);
-// publish a frame's FrameVar in its slot (dst) and zero the slot's work-queue counters
-hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, int* queue, hipStream_t s);
+// the running-mean updates of nFrames pipelined frames over the rank's owned pixels (PackParams
+// mapping), in frame order: for f = 0 .. nFrames-1, accum = mix(accum, col + f * colStride,
+// 1 / (frameCounter + f + 1)) (IS:868-871, pass2.fsh:15) -- each pixel read and written once
+hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, size_t colStride, int nFrames,
+                     uint32_t frameCounter, hipStream_t s);
 
 }  // namespace pt

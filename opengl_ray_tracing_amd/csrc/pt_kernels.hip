@@ -18,9 +18,7 @@
 //    instead of the reference's three); triangles as 64-byte records with the
 //    precomputed unit normal and plane offset.
 #include <hip/hip_runtime.h>
-#include <hip/hip_fp16.h>
 
-#include <cstdlib>
 #include <stdint.h>
 
 #include "pt_device.h"
@@ -168,48 +166,20 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
   const uint32_t gi = grayCode(frameCounter + 1u);  // frameCounter = the sample index here
   float cpu, cpv;
   cranleyPattersonShift(px, py, cpu, cpv);
-#if PT_LIGHT_PREFETCH
-  // The light sample of a bounce depends only on the RNG state at its start
-  // (r1, r2 -> cache texel -> direction -> env texel), which is known one
-  // bounce early: bounce b + 1's cache texel is fetched before bounce b's
-  // shadow walk and its env texel before the closest-hit walk, so neither
-  // dependent Infinity-Cache fetch sits on the path's chain. Same operations
-  // on the same values; the RNG is advanced where the reference draws.
-  V3 LdirN;
-  float4 texN;
-  float wN;
-  {
-    uint32_t s = seed;
-    const float a = randf(s);
-    const float b = randf(s);
-    LdirN = hdrDirFromCache(hdrCacheTexel(env, a, b));
-    texN = hdrTexelOf(env, LdirN, wN);
-  }
-#endif
   for (int bounce = 0; bounce < maxBounce; bounce++) {
     const V3 V = -hit.viewDir;
     const V3 N = hit.N;
     // (1) light sample IS:772-789
     const float r1 = randf(seed);
     const float r2 = randf(seed);
-#if PT_LIGHT_PREFETCH
-    (void)r1;
-    (void)r2;
-    const V3 Ldir = LdirN;
-#else
     const V3 Ldir = sampleHdrDir(env, r1, r2);
-#endif
     if (count) C.texels++;
     const bool tryLight = dot(N, Ldir) > 0.0f;
     V3 lightC = v3(0, 0, 0);
     if (tryLight) {
       V3 color;
       float pdf_light;
-#if PT_LIGHT_PREFETCH
-      hdrColorPdfOf(env, texN, wN, color, pdf_light);
-#else
       hdrColorPdf(env, Ldir, color, pdf_light);
-#endif
       V3 f_r = brdfIso(V, N, Ldir, hit.m);
       float pdf_brdf = brdfPdf(V, N, Ldir, hit.m);
       float mis_weight = misWeight(pdf_light, pdf_brdf);
@@ -225,26 +195,11 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
     const float NdotL = dot(N, L);
     const V3 f_r = brdfIso(V, N, L, hit.m);
     const float pdf_brdf = brdfPdf(V, N, L, hit.m);
-#if PT_LIGHT_PREFETCH
-    float2 cacheN = make_float2(0.0f, 0.0f);
-    if (bounce + 1 < maxBounce) {
-      uint32_t s = seed;
-      const float a = randf(s);
-      const float b = randf(s);
-      cacheN = hdrCacheTexel(env, a, b);
-    }
-#endif
     if (tryLight && !tr.occluded(hit.P, Ldir)) {
       Lo = Lo + lightC;
       if (count) C.texels += 2;
     }
     if (NdotL <= 0.0f) break;
-#if PT_LIGHT_PREFETCH
-    if (bounce + 1 < maxBounce) {
-      LdirN = hdrDirFromCache(cacheN);
-      texN = hdrTexelOf(env, LdirN, wN);
-    }
-#endif
     Hit nh;
     bool isHit = tr.closest(hit.P, L, nh);
     if (pdf_brdf <= 0.0f) break;
@@ -283,13 +238,12 @@ __device__ __forceinline__ V3 cameraRay(const RenderParams& p, uint32_t sampleIn
   return normalize(dir);
 }
 
-// f: the frame the pixel belongs to (its sample index and colour buffer; FrameVar)
-__device__ __forceinline__ void accumulate(const RenderParams& p, const FrameVar& f, int px, int py, V3 color, Counters& C,
+// f: the frame the pixel belongs to (its sample index and colour buffer)
+__device__ __forceinline__ void accumulate(const RenderParams& p, const FrameRef& f, int px, int py, V3 color, Counters& C,
                                            bool count) {
   float4* col = f.col;
-  if (!count && col) {  // pipelined frame: the sample colour, mixed into the running mean in frame order
-    // (by another CU's wave, maybe in this launch: a write-through store, completeItem)
-    stCoherent(col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
+  if (!count && col) {  // pipelined frame: the sample colour, mixed into the running mean in frame order (mixKernel)
+    stStream(col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
     return;
   }
   float4* a = p.accum + (size_t)py * p.width + px;
@@ -301,7 +255,7 @@ __device__ __forceinline__ void accumulate(const RenderParams& p, const FrameVar
 
 // the camera ray's closest hit; a miss is finished here (sky colour accumulated)
 template <bool CULL, bool COUNT>
-__device__ __forceinline__ int primaryPixel(const RenderParams& p, const FrameVar& f, int px, int py, Stack& st,
+__device__ __forceinline__ int primaryPixel(const RenderParams& p, const FrameRef& f, int px, int py, Stack& st,
                                             Counters& C, const float4* top, float& t) {
   uint32_t seed;
   const V3 dir = cameraRay(p, f.sampleIndex, px, py, seed);
@@ -320,7 +274,7 @@ __device__ __forceinline__ int primaryPixel(const RenderParams& p, const FrameVa
 // one packet (tracePacket); a ray that met an exact tie is retraced in the
 // reference order. All 64 lanes call it; valid marks the lanes with a pixel.
 template <bool CULL>
-__device__ __forceinline__ int primaryPacket(const RenderParams& p, const FrameVar& f, int px, int py, bool valid,
+__device__ __forceinline__ int primaryPacket(const RenderParams& p, const FrameRef& f, int px, int py, bool valid,
                                              Stack& st, Counters& C, const float4* top, PacketEntry* pstack, float& t) {
   uint32_t seed;
   const V3 dir = cameraRay(p, f.sampleIndex, valid ? px : 0, valid ? py : 0, seed);
@@ -421,9 +375,11 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, const FrameV
 __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   __shared__ float4 s_tri[PT_PASS_BIN_CAP * 4];
   __shared__ int s_idx[PT_PASS_BIN_CAP];
-  const int w = blockIdx.x;
+  // block b: tile b / nFrames of frame b % nFrames (a batch's frames of one tile side by side)
+  const int fr = (int)(blockIdx.x % (unsigned)p.nFrames);
+  const int w = (int)(blockIdx.x / (unsigned)p.nFrames);
   const int lane = threadIdx.x;
-  if (p.zeroQueue && w == 0)  // the frame kernel's work-queue counters, zeroed for it (it runs next on this stream)
+  if (p.zeroQueue && blockIdx.x == 0)  // the frame kernel's work-queue counters, zeroed for it (it runs next on this stream)
     for (int q = lane; q < NUM_QUEUES; q += 64) p.queue[q * CTL_LINE_INTS] = 0;
   const int sub = p.shardSize >> 3;
   const int j = w / p.shardTiles, s = w - j * p.shardTiles;
@@ -439,9 +395,10 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
     b1 = p.binStart[ty * p.binTilesX + tx + 1];
   }
   const int n = b1 - b0;
-  int2* out = p.primHit + (size_t)py * p.width + px;
-  FrameVar fp{};  // this launch's frame (accumulate's colour buffer)
-  fp.col = p.col;
+  int2* out = p.primHit + (size_t)fr * p.colStride + (size_t)py * p.width + px;
+  FrameRef fp;  // this block's frame (accumulate's colour buffer)
+  fp.col = p.col ? p.col + (size_t)fr * p.colStride : nullptr;
+  fp.sampleIndex = p.sampleIndex + (uint32_t)fr * p.sampleStride;
   if (n > PT_PASS_BIN_CAP) {  // the frame kernel traces this tile's camera rays (the megakernel as a packet)
     if (valid) *out = make_int2(PRIM_TILE, 0);
     return;
@@ -453,7 +410,7 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   }
   __syncthreads();
   uint32_t seed;
-  const V3 dir = cameraRay(p, p.sampleIndex, valid ? px : 0, valid ? py : 0, seed);
+  const V3 dir = cameraRay(p, fp.sampleIndex, valid ? px : 0, valid ? py : 0, seed);
   const V3 eye = v3(p.eye[0], p.eye[1], p.eye[2]);
   float tbest = PT_INF;
   int best = -1;
@@ -487,13 +444,13 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
 
 hipError_t launchPrimary(const RenderParams& p, hipStream_t s) {
   if (!p.primHit || !p.binStart || p.numItems <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(primaryKernel, dim3(p.numItems), dim3(64), 0, s, p);
+  hipLaunchKernelGGL(primaryKernel, dim3((unsigned)p.numItems * (unsigned)p.nFrames), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 
 // the rest of the path of a pixel whose camera ray hit triangle tri at t
 template <int INTEG, bool CULL, bool COUNT>
-__device__ __forceinline__ void finishPixel(const RenderParams& p, const FrameVar& f, int px, int py, int tri, float t,
+__device__ __forceinline__ void finishPixel(const RenderParams& p, const FrameRef& f, int px, int py, int tri, float t,
                                             Stack& st, Counters& C, const float4* top) {
   Tracer<CULL, COUNT> tr{p.scene, st, C, top};
   uint32_t seed;
@@ -861,86 +818,6 @@ __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
   return v;
 }
 
-// ------------------------------------------------ running mean inside the frame kernel
-// (RenderParams::tileDone / mixState; pt_runtime.cpp "frames in flight")
-__device__ __forceinline__ void tileOrigin(const RenderParams& p, int w, int& px0, int& py0) {
-  const int sub = p.shardSize >> 3;
-  const int j = w / p.shardTiles, s = w - j * p.shardTiles;
-  const int g = j * p.world + p.rank;
-  const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
-  px0 = gx * p.shardSize + (s % sub) * 8;
-  py0 = gy * p.shardSize + (s / sub) * 8;
-}
-// Frame `seq`'s item of tile w has written the sample colours of its pixels (valid lanes).
-// When that completes the tile for the frame, the wave brings the tile's running mean
-// (IS:868-871) up to date in frame order: it mixes the frame in if every earlier frame is
-// already mixed into the tile -- else the wave that mixes the frame before it will -- and
-// then each later frame that has already completed the tile. A per-tile lock word
-// (mixState = 2 * next frame to mix, + 1 while locked) admits one wave at a time and only for
-// the next frame in order. The completer counts, then tries the lock; the mixer unlocks,
-// then reads the next frame's count; each waits for its first access to complete before the
-// second, so a frame that completes the tile while another wave holds the lock is seen by
-// one of the two. Colours and the mean cross CUs as write-through (sc1) stores drained before
-// the count or the unlock and sc1 loads after it (stCoherent / ldCoherent): no cache
-// maintenance, and no wave ever waits for another. The image is the one of frames mixed
-// one after another (the same mixf, the same order).
-__device__ __forceinline__ void completeItem(const RenderParams& p, const FrameVar& fv, uint32_t seq, int w,
-                                             bool valid) {
-  const int lane = __lane_id();
-  const uint32_t D1 = (uint32_t)p.depth + 1u;
-  const int n = __popcll(__ballot(valid));
-  int px0, py0;
-  tileOrigin(p, w, px0, py0);
-  const int need = (px0 < p.width && py0 < p.height) ? min(8, p.width - px0) * min(8, p.height - py0) : 0;
-  if (need == 0) return;  // a tile of a shard wholly outside the image: no pixels, nothing to mix
-  drainStores();          // the wave's colour stores, before its count
-  int done = 0;
-  if (lane == 0)
-    done = __hip_atomic_fetch_add(p.tileDone + (size_t)(seq % D1) * p.numItems + w, n, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT) + n;
-  if (__shfl(done, 0, 64) != need) return;
-  const int px = px0 + (lane & 7), py = py0 + (lane >> 3);
-  const bool in = px < p.width && py < p.height;
-  const size_t i = (size_t)py * p.width + px;
-  uint32_t g = seq;
-  // at most the frames in flight after seq can have completed the tile (bounded, come what may)
-  for (uint32_t k = 0; k <= (uint32_t)p.depth; k++) {
-    unsigned old = 2u * g;
-    if (lane == 0)
-      __hip_atomic_compare_exchange_strong(p.mixState + w, &old, 2u * g + 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    if ((unsigned)__shfl((int)old, 0, 64) != 2u * g) return;  // not g's turn yet, or locked: that wave mixes g
-    const float4* col = fv.col;
-    uint32_t fc = fv.frameCounter;
-    if (g != seq) {  // a later frame that completed the tile first: its published FrameVar
-      const FrameVar* v = p.frameVars + g % (uint32_t)p.depth;
-      const unsigned long long cb =
-          __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&v->col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      col = (const float4*)((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cb) |
-                            (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(cb >> 32)) << 32);
-      fc = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)__hip_atomic_load(&v->frameCounter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    if (in) {  // mixKernel's update of one pixel
-      const float4 c = ldCoherent(col + i);
-      const float4 a = ldCoherent(p.accum + i);
-      const float wt = 1.0f / (float)(fc + 1u);
-      stCoherent(p.accum + i, make_float4(mixf(a.x, c.x, wt), mixf(a.y, c.y, wt), mixf(a.z, c.z, wt), 1.0f));
-    }
-    drainStores();  // the tile's new mean, before the unlock
-    int next = 0;
-    if (lane == 0) {
-      __hip_atomic_store(p.tileDone + (size_t)(g % D1) * p.numItems + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.mixState + w, 2u * (g + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      drainStores();  // the unlock, before the next frame's count is read
-      next = __hip_atomic_load(p.tileDone + (size_t)((g + 1u) % D1) * p.numItems + w, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (__shfl(next, 0, 64) != need) return;  // the next frame has not completed the tile: its completer mixes it
-    g++;
-  }
-}
-
 // WAVES > 0: compiled for that many waves per SIMD (the latency-bound large
 // scenes' variant, pt_runtime.cpp renderFrame)
 template <int INTEG, bool CULL, bool COUNT, int WAVES = 0>
@@ -958,7 +835,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     const bool w4 = PT_WIDE4 == 2 && !COUNT && p.scene.fast;  // the 4-wide tree's top
     const float4* src = w4 ? p.scene.fbvh4 : p.scene.fast ? p.scene.fbvh : p.scene.bvh;  // the tree traversed first
     // the copy's size from the staged tree's own record kind (never the other tree's: DESIGN.md §8)
-    const int n = w4 ? p.scene.f4nTop * W4_NODE_F4 : p.scene.fast ? p.scene.fnTop * nodeF4<FAST_KIND>() : p.scene.nTop * 4;
+    const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.fast ? p.scene.fnTop * 4 : p.scene.nTop * 4;
     for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
   }
   __syncthreads();
@@ -983,30 +860,13 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
   // queue and running them 64 at a time keeps every lane busy, but it mixes
   // tiles: 64-path batches made c2 0.77 ms instead of 0.55, 32-path batches
   // 0.59 -- the coherence of one tile's rays is worth more than full lanes.)
-  const int waveId = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6), numWaves = gridDim.x * (BLOCK / 64);
-  int dealt = 0;  // statically dealt items taken (band order)
-  // this launch's frame: its sample index, colour buffer and weight (completeItem, accumulate)
-  FrameVar fv;
-  fv.col = p.col;
-  fv.sampleIndex = p.sampleIndex;
-  fv.frameCounter = p.frameCounter;
-  auto claim = [&]() -> int {
-    if (p.staticItems > 0) {
-      const int t = waveId + dealt * numWaves;
-      if (t < p.staticItems) {
-        dealt++;
-        return t;
-      }
-      const int it = cur.next(p.queue, p.dynPerQueue, p.numItems - p.staticItems, home);
-      return it < 0 ? it : p.staticItems + it;
-    }
-    return cur.next(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
-  };
-  int item = claim();
+  int fr = 0;  // the claimed item's frame in the launch's batch
+  int item = cur.next(p.queue, p.perQueue, p.numItems, home, fr, p.nFrames, p.tileOrder, p.orderCap);
   while (item >= 0) {
-#if PT_CLAIM_AHEAD
-    cur.claimAhead(p.queue, home);
-#endif
+    // the item's frame: its sample index and colour buffer (accumulate)
+    FrameRef fv;
+    fv.col = p.col ? p.col + (size_t)fr * p.colStride : nullptr;
+    fv.sampleIndex = p.sampleIndex + (uint32_t)fr * p.sampleStride;
     const int w = itemTile(item);
     const long long t0 = COUNT ? 0 : clock64();
 #if PT_WAVE_TRACE
@@ -1023,7 +883,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
     const bool valid = lane < nLanes && px < p.width && py < p.height;
     if (!COUNT && p.primHit) {  // camera rays already traced by primaryKernel
-      const int2 h = valid ? p.primHit[(size_t)py * p.width + px] : make_int2(PRIM_MISS, 0);
+      const int2 h = valid ? p.primHit[(size_t)fr * p.colStride + (size_t)py * p.width + px] : make_int2(PRIM_MISS, 0);
       int tri = h.x;
       float t = __int_as_float(h.y);
       if (__ballot(valid && tri == PRIM_TILE)) {  // wave-uniform: the whole tile
@@ -1045,7 +905,6 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
       const int tri = primaryPixel<CULL, COUNT>(p, fv, px, py, st, C, top, t);
       if (tri >= 0) finishPixel<INTEG, CULL, COUNT>(p, fv, px, py, tri, t, st, C, top);
     }
-    if (!COUNT && p.mixState) completeItem(p, fv, p.seq, w, valid);
     if (!COUNT && p.tileCost && lane == 0) {
       const int dt = (int)min(clock64() - t0, (long long)0x3fffffff);
       atomicAdd(p.tileCost + w, dt);
@@ -1067,11 +926,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAV
       wLongestAt = (unsigned long long)__shfl(px, 0, 64) << 16 | (unsigned long long)__shfl(py, 0, 64);
     }
 #endif
-#if PT_CLAIM_AHEAD
-    item = cur.nextAhead(p.queue, p.perQueue, p.numItems, home, p.tileOrder, p.orderCap);
-#else
-    item = claim();
-#endif
+    item = cur.next(p.queue, p.perQueue, p.numItems, home, fr, p.nFrames, p.tileOrder, p.orderCap);
   }
 #if PT_WAVE_TRACE
   if (p.waveTrace && lane == 0) {
@@ -1215,17 +1070,23 @@ __global__ void displayUnpackKernel(DisplayUnpack d, uchar4* image) {
     image[(size_t)py * p.width + px] = make_uchar4(src[3 * k], src[3 * k + 1], src[3 * k + 2], 255);
 }
 
-// the running mean of a pipelined frame (accumulate's update, deferred to frame order)
-__global__ void mixKernel(PackParams p, float4* accum, const float4* col, uint32_t frameCounter) {
+// the running means of a batch of pipelined frames (accumulate's update, deferred to frame
+// order): frame f's colours at col + f * colStride, its weight 1 / (frameCounter + f + 1); the
+// pixel's mean after each frame is the one serial frames store (mixf of the same floats)
+__global__ void mixKernel(PackParams p, float4* accum, const float4* col, size_t colStride, int nFrames,
+                          uint32_t frameCounter) {
   long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= p.count) return;
   int px, py;
   if (!packedPixel(p, k, px, py)) return;
   const size_t i = (size_t)py * p.width + px;
-  const float4 c = ldStream(col + i);
-  const float4 old = ldStream(accum + i);
-  const float w = 1.0f / (float)(frameCounter + 1u);
-  stStream(accum + i, make_float4(mixf(old.x, c.x, w), mixf(old.y, c.y, w), mixf(old.z, c.z, w), 1.0f));
+  float4 a = ldStream(accum + i);
+  for (int f = 0; f < nFrames; f++) {
+    const float4 c = ldStream(col + (size_t)f * colStride + i);
+    const float w = 1.0f / (float)(frameCounter + (uint32_t)f + 1u);
+    a = make_float4(mixf(a.x, c.x, w), mixf(a.y, c.y, w), mixf(a.z, c.z, w), 1.0f);
+  }
+  stStream(accum + i, a);
 }
 
 // include/pt_fmath.h evaluated on the device (diagnostics; bit-equality with the host)
@@ -1299,6 +1160,30 @@ hipError_t launchBasic(const BasicParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+__global__ void basicWidenKernel(const float4* accum, double* image, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 a = accum[i];
+  image[3 * i] = (double)a.x;
+  image[3 * i + 1] = (double)a.y;
+  image[3 * i + 2] = (double)a.z;
+}
+__global__ void basicNarrowKernel(const double* image, float4* accum, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  accum[i] = make_float4((float)image[3 * i], (float)image[3 * i + 1], (float)image[3 * i + 2], 1.0f);  // basicKernel's store
+}
+hipError_t launchBasicWiden(const float4* accum, double* image, long n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(basicWidenKernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, accum, image, n);
+  return hipGetLastError();
+}
+hipError_t launchBasicNarrow(const double* image, float4* accum, long n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(basicNarrowKernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, image, accum, n);
+  return hipGetLastError();
+}
+
 hipError_t launchTonemap(const float4* accum, float* rgb, int n, float limit, float gamma, hipStream_t s) {
   hipLaunchKernelGGL(tonemapKernel, dim3((n + 255) / 256), dim3(256), 0, s, accum, rgb, n, limit, gamma);
   return hipGetLastError();
@@ -1315,29 +1200,11 @@ hipError_t launchPack(const PackParams& p, const float4* accum, float* packed, h
   hipLaunchKernelGGL(packKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, packed);
   return hipGetLastError();
 }
-hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, uint32_t frameCounter, hipStream_t s) {
-  if (p.count <= 0) return hipSuccess;
-  static const int bs = [] {
-    const char* e = std::getenv("PT_MIX_BLOCK");
-    const int v = e ? std::atoi(e) : 256;
-    return v == 64 || v == 128 || v == 256 || v == 512 || v == 1024 ? v : 256;
-  }();
-  hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + bs - 1) / bs)), dim3(bs), 0, s, p, accum, col, frameCounter);
-  return hipGetLastError();
-}
-// A frame's FrameVar published in its slot (read by earlier frames' waves during their
-// launches: write-through 8-byte stores), and the slot's work-queue counters zeroed: one
-// 64-thread launch instead of a FrameVar copy and a memset
-__global__ void frameVarKernel(FrameVar v, FrameVar* dst, int* queue) {
-  static_assert(sizeof(FrameVar) % 8 == 0, "FrameVar in 8-byte words");
-  const int t = threadIdx.x;
-  if (t < (int)(sizeof(FrameVar) / 8))
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + t, reinterpret_cast<const unsigned long long*>(&v)[t],
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t < NUM_QUEUES) queue[t * CTL_LINE_INTS] = 0;
-}
-hipError_t launchFrameVar(const FrameVar& v, FrameVar* dst, int* queue, hipStream_t s) {
-  hipLaunchKernelGGL(frameVarKernel, dim3(1), dim3(64), 0, s, v, dst, queue);
+hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, size_t colStride, int nFrames,
+                     uint32_t frameCounter, hipStream_t s) {
+  if (p.count <= 0 || nFrames <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, col, colStride,
+                     nFrames, frameCounter);
   return hipGetLastError();
 }
 hipError_t launchDisplayPack(const PackParams& p, const float4* accum, float limit, float gamma, uint8_t* packed,
@@ -1360,31 +1227,6 @@ hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image,
   if (world < 2 || most <= 0) return hipSuccess;
   hipLaunchKernelGGL(displayUnpackKernel, dim3((unsigned)((most + 255) / 256), (unsigned)(world - 1)), dim3(256), 0, s,
                      d, image);
-  return hipGetLastError();
-}
-__global__ void halfNodes4Kernel(const float4* full, int n, float4* half) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4* r = full + (size_t)i * W4_F4;
-  auto pk = [](float x, float y, bool up) {  // two planes as halves, rounded outward
-    const __half a = up ? __float2half_ru(x) : __float2half_rd(x), b = up ? __float2half_ru(y) : __float2half_rd(y);
-    return __uint_as_float((uint32_t)__half_as_ushort(a) | (uint32_t)__half_as_ushort(b) << 16);
-  };
-  float w[12];
-  for (int a = 0; a < 6; a++) {  // lo.x, lo.y, lo.z, hi.x, hi.y, hi.z
-    const float4 v = r[a];
-    w[2 * a] = pk(v.x, v.y, a >= 3);
-    w[2 * a + 1] = pk(v.z, v.w, a >= 3);
-  }
-  float4* o = half + (size_t)i * 4;
-  o[0] = make_float4(w[0], w[1], w[2], w[3]);
-  o[1] = make_float4(w[4], w[5], w[6], w[7]);
-  o[2] = make_float4(w[8], w[9], w[10], w[11]);
-  o[3] = r[6];
-}
-hipError_t launchHalfNodes4(const float4* full, int n, float4* half, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(halfNodes4Kernel, dim3((n + 255) / 256), dim3(256), 0, s, full, n, half);
   return hipGetLastError();
 }
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s) {

@@ -64,6 +64,7 @@ enum : int { K_NONE = 0, K_PRIMARY = 1, K_BOUNCE = 2, K_SHADOW = 3 };
 
 struct PathState {
   int px, py;
+  int fr;        // the pixel's frame in the launch's batch (RenderParams::nFrames)
   int kind;      // the ray in flight (K_*)
   int bounce;    // bounce index of the K_BOUNCE / K_SHADOW ray
   uint32_t seed;
@@ -77,9 +78,15 @@ struct PathState {
   bool haveB;    // MIS: a BRDF ray follows the shadow ray
 };
 
-__device__ __forceinline__ void writeAccum(const RenderParams& p, int px, int py, V3 color) {
+__device__ __forceinline__ uint32_t sampleOf(const RenderParams& p, const PathState& s) {
+  return p.sampleIndex + (uint32_t)s.fr * p.sampleStride;
+}
+
+__device__ __forceinline__ void writeAccum(const RenderParams& p, const PathState& s, V3 color) {
+  const int px = s.px, py = s.py;
   if (p.col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in frame order
-    stStream(p.col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
+    stStream(p.col + (size_t)s.fr * p.colStride + (size_t)py * p.width + px,
+             make_float4(color.x, color.y, color.z, 1.0f));
     return;
   }
   float4* a = p.accum + (size_t)py * p.width + px;
@@ -91,7 +98,7 @@ __device__ __forceinline__ void writeAccum(const RenderParams& p, int px, int py
 // main IS:846-850: seed and camera ray of pixel (px, py)
 __device__ __forceinline__ void startPath(const RenderParams& p, PathState& s) {
   const int W = p.width, H = p.height;
-  s.seed = ((uint32_t)s.px * 1973u + (uint32_t)s.py * 9277u + p.sampleIndex * 26699u) | 1u;
+  s.seed = ((uint32_t)s.px * 1973u + (uint32_t)s.py * 9277u + sampleOf(p, s) * 26699u) | 1u;
   float pixx = (float)(2 * s.px + 1) / (float)W - 1.0f;
   float pixy = (float)(2 * s.py + 1) / (float)H - 1.0f;
   float ax = (randf(s.seed) - 0.5f) / (float)W;
@@ -148,7 +155,7 @@ __device__ __forceinline__ bool continueFromHit(const RenderParams& p, PathState
     s.shC = (c * dot(N, L)) / pdf_light;
     shadow = true;
   }
-  const uint32_t gi = grayCode(p.sampleIndex + 1u);
+  const uint32_t gi = grayCode(sampleOf(p, s) + 1u);
   float u = sobolf(2u * (uint32_t)nb, gi);
   float v = sobolf(2u * (uint32_t)nb + 1u, gi);
   cranleyPatterson(s.px, s.py, u, v);
@@ -256,12 +263,12 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   // the top of the uploaded tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
   constexpr int TOP4 = regenTop4W(WAVES);
-  constexpr int TOPF4 = (W4 && TOP4 * W4_NODE_F4 > LDS_NODES * 4) ? TOP4 * W4_NODE_F4 : LDS_NODES * 4;
+  constexpr int TOPF4 = (W4 && TOP4 * W4_F4 > LDS_NODES * 4) ? TOP4 * W4_F4 : LDS_NODES * 4;
   __shared__ float4 s_nodes[TOPF4];
   {
     const bool w4 = W4 && p.scene.fast;
     const float4* src = w4 ? p.scene.fbvh4 : p.scene.bvh;
-    const int n = w4 ? p.scene.f4nTop * W4_NODE_F4 : p.scene.nTop * 4;  // the staged tree's own record size
+    const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.nTop * 4;  // the staged tree's own record size
     for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
   }
   __syncthreads();
@@ -276,12 +283,13 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   const int sub = p.shardSize >> 3;
   TileCursor cur;     // wave-uniform
   int tile = -1;      // current 8x8 wave tile (wave-uniform)
+  int tileFr = 0;     // its frame in the launch's batch (wave-uniform)
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
   bool active = false;
   bool walking = false;  // PT_REGEN_YIELD: the lane's ray has a walk in progress (w, st)
   Walk4 w;
   PathState s;
-  s.px = s.py = 0;
+  s.px = s.py = s.fr = 0;
   s.kind = K_NONE;
 #if PT_WAVE_TRACE
   // diagnostics build: {start, end, tiles | last lone lane's pixel << 32, last successful claim,
@@ -295,7 +303,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
       const unsigned long long idle = __ballot(!active);
       if (idle == 0) break;
       if (cursor >= 64) {
-        const int item = cur.next(p.queue, p.perQueue, p.numItems, home, nullptr);
+        const int item = cur.next(p.queue, p.perQueue, p.numItems, home, tileFr, p.nFrames);
         if (item < 0) break;  // no tiles left for this wave
         tile = item;
         cursor = 0;
@@ -314,16 +322,17 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
         if (px < p.width && py < p.height) {
           s.px = px;
           s.py = py;
+          s.fr = tileFr;
           startPath(p, s);
           active = true;
           if (p.primHit) {  // the camera ray's result from the camera-ray pass (primaryKernel)
-            const int2 h = p.primHit[(size_t)py * p.width + px];
+            const int2 h = p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px];
             if (h.x == PRIM_MISS) {
               active = false;  // a sky pixel, finished by the pass: the lane takes another
             } else if (h.x >= 0) {
               V3 color;
               if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
-                writeAccum(p, s.px, s.py, color);
+                writeAccum(p, s, color);
                 active = false;
               }
             }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
@@ -375,7 +384,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
     }
     V3 color;
     if (!advance<INTEG>(p, s, tri, t, color)) {
-      writeAccum(p, s.px, s.py, color);
+      writeAccum(p, s, color);
       active = false;
     }
   }

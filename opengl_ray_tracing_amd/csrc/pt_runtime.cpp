@@ -29,31 +29,39 @@
 using namespace pt;
 
 static constexpr int EV_RING = 64;
-// Frames in flight: the default megakernel's frame g (its pipeline sequence
-// number) runs on slot stream g % depth (8 by default) with its own work queues,
-// overflow stack, tile order and camera-ray results, and writes its sample colours
-// to colour buffer g % (depth + 1). While other frames are in flight its persistent
-// grid is 1/depth of residency (renderOne), so the frames in flight share the GPU by
-// space: their waves are resident together, and a frame whose last long paths keep a
-// few waves busy leaves the rest of the machine to the others. Its running-mean
-// update (mixKernel) runs on the caller's stream, in frame order, once the frame's
-// kernel has ended: the accumulation is updated in frame order, the image is bit for
-// bit the one of serial frames, and whatever the caller queues behind a frame (pack,
-// download, tonemap) follows its update with no further cross-queue wait. No frame
-// kernel waits for a mix except the one of the frame depth + 1 back, whose colour
-// buffer it reuses. (Measured alternatives, DESIGN.md 4: a separate mix stream is
-// twice as slow at small shares -- each mix waited on two ~25 us cross-queue signals
-// in a chain from mix to mix; and with full-residency grids a mix waits for a CU slot
-// behind the next frame's persistent kernel, ~250 us on c2, which made deeper
-// pipelines slower, not faster.)
+// Frames in flight: the default megakernel's (or regen kernel's) launch g (its pipeline
+// sequence number) runs on slot stream g % depth (8 by default) with its own work queues,
+// overflow stack, tile order and camera-ray results, and writes its sample colours to colour
+// buffer g % (2 * depth + 1). While other launches are in flight its persistent grid is 1.5 /
+// depth of residency (renderOne), so the frames in flight share the GPU by space: their waves
+// are resident together, and a frame whose last long paths keep a few waves busy leaves the
+// rest of the machine to the others. Its running-mean update (mixKernel) runs on the caller's
+// stream, in frame order, once the launch's kernel has ended: the accumulation is updated in
+// frame order, the image is bit for bit the one of serial frames, and whatever the caller
+// queues behind a frame (pack, download, tonemap) follows its update with no further
+// cross-queue wait. No launch waits for a mix except the one of the launch 2 * depth + 1 back,
+// whose colour buffer it reuses.
+//
+// A launch may render a batch of consecutive frames of one camera (pt_render_frames_async,
+// RenderParams::nFrames): every frame's colours in its own part of the colour buffer, and one
+// mixKernel folds them into the running mean pixel by pixel in frame order. A small screen-tile
+// share (1/8 of the image) gives one frame too little work to fill the machine; a batch of
+// tile_world frames per launch is about one whole image's work, and the chain of running-mean
+// updates on the caller's stream -- one cross-queue wait and one launch per update, which set
+// an 8-way share's frame period before -- has one link per batch.
+// (Measured alternatives, DESIGN.md 4: a separate mix stream is twice as slow at small
+// shares -- each mix waited on two ~25 us cross-queue signals in a chain from mix to mix; and
+// with full-residency grids a mix waits for a CU slot behind the next frame's persistent
+// kernel, ~250 us on c2, which made deeper pipelines slower, not faster.)
 #ifndef PT_PIPE
 #define PT_PIPE 8  // frames in flight (PT_PIPE_DEPTH overrides; capped by the hardware queues)
 #endif
 static constexpr int PIPE = MAX_SLOTS;      // most frames in flight
-// colour buffers: a frame reuses the buffer of the frame 2 * depth + 1 back (the in-kernel running
-// mean's protocol: depth + 1 back), whose running-mean update is then long done -- with depth + 1 the
-// wait made a slot's next frame follow the running-mean update of the previous frame on another slot
-// (two cross-queue hops), and an N = 8 share of c2 kept only ~3 of its 8 frames in flight
+static constexpr int MAX_BATCH = 16;        // most frames per launch (pt_render_frames_async)
+// colour buffers: a launch reuses the buffer of the launch 2 * depth + 1 back, whose running-mean
+// update is then long done -- with depth + 1 the wait made a slot's next frame follow the
+// running-mean update of the previous frame on another slot (two cross-queue hops), and an N = 8
+// share of c2 kept only ~3 of its 8 frames in flight
 static constexpr int COLS = 2 * MAX_SLOTS + 1;
 static_assert(PT_PIPE >= 1 && PT_PIPE <= PIPE, "PT_PIPE: 1..MAX_SLOTS");
 static_assert(PIPE * NUM_QUEUES * CTL_LINE_INTS * 4 <= (int)CTL_STATS, "queue counters of every slot fit the control block");
@@ -79,6 +87,7 @@ struct pt_ctx {
   double msTotal = 0.0;         // summed device time of the folded launches since the reset
   float msLast = 0.0f;          // device time of the last folded launch
   int launches = 0;             // render launches since the reset
+  long long frames = 0;         // frames those launches rendered (a batch launch renders several)
   int tagSlot = -1;             // probe slot for the launch being issued (probePolicy)
   int numCU = 0;
   // scene
@@ -145,36 +154,17 @@ struct pt_ctx {
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
   int pipeDepthBase = PT_PIPE;              // ... as chosen at creation (uploadScene may lower it for large scenes)
   bool pipeDepthFixed = false;              // PT_PIPE_DEPTH set: no scene-dependent choice
-  bool gridShare = true;                    // frames in flight split the persistent grid (PT_GRID_SHARE=0: not)
-  // % of residency the frames in flight split (PT_GRID_PCT): 150 -- each frame's grid half again its
-  // equal share, so a frame finishing early leaves waves of the others ready to take its place --
-  // measured against 100 / 200 / 300 with the bench line as the driver runs it (20 frames from an
-  // idle GPU): c2 0.285 / 0.262 / 0.266 / 0.289 ms per frame (100 / 150 / 200 / 300), c4 0.413 /
-  // 0.360 / 0.367 / 0.385; 100 frames: c2 0.246 (100) vs 0.245 (200), c4 0.349 vs 0.332
-  int gridPct = 150;
-  // frame streams at the lowest stream priority (PT_SLOT_PRIORITY=1; measured slower: an N = 8 share
-  // of c2 0.065 -> 0.105 ms per frame)
-  bool slotPriority = false;
-  // PT_GRID_ALWAYS=1: a frame's grid is its share even with no other frame in flight (bench line, 20
-  // frames from idle: c2 0.2532 / 0.2532 -> 0.2476 / 0.2578 ms, c4 0.373 / 0.368 -> 0.370 / 0.365: noise)
-  bool gridAlways = false;
-  // the running mean updated tile by tile inside the frame kernels (renderKernel completeItem;
-  // PT_KERNEL_MIX=1; off: mixKernel per frame on the caller's stream): per colour buffer and tile
-  // the pixels written, per tile the lock word (2 x next frame to mix); valid from frame
-  // protoNext on while protoValid, re-initialised (after every earlier frame) otherwise
-  bool kernelMix = false;
+  // Frames of one pt_render_frames_async call rendered per launch (RenderParams::nFrames), at most:
+  // pt_config.frame_batch, else as many as make one launch about a whole image's work (tile_world
+  // frames of a screen-tile share, up to MAX_BATCH). Probe frames and frameCounter 0 run alone.
+  int batchCap = 1;
+  int colCap[COLS] = {};                    // frames each colour buffer holds
+  int primCap[PIPE] = {};                   // frames each slot's camera-ray results hold
   // the large-scene path (regen kernel at 4 waves/SIMD, 4-wide walk with dynamic ray fetch,
   // camera-ray pass) on scenes of any size: -1 = for the Lambert integrator (c2 0.342 ->
   // 0.251 ms/frame; MIS c4 0.355 -> 0.468, Disney-MIS c3 0.160 -> 0.163: those keep the
-  // megakernel), 1 = every integrator, 0 = large scenes only (PT_REGEN_WIDE)
+  // megakernel); PT_FLAG_REGEN / PT_FLAG_MEGAKERNEL choose per context
   int regenWide = -1;
-  int* d_tileDone = nullptr;
-  unsigned* d_mixState = nullptr;
-  bool protoValid = false;
-  unsigned long long protoNext = 0;
-  hipEvent_t protoInit = nullptr, callerMark = nullptr;
-  unsigned protoGen = 0, protoGenSeen[MAX_SLOTS] = {};
-  FrameVar* d_frameVars = nullptr;          // per slot: the published FrameVar (frameVarKernel)
   hipStream_t slotStream[PIPE] = {};
   hipEvent_t kernelDone[PIPE] = {};         // slot's last frame kernel (+ reorder) ended
   bool slotBusy[PIPE] = {};                 // kernelDone[k] has been recorded since the last sync
@@ -341,17 +331,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   hipDeviceProp_t prop;
   CKC(hipGetDeviceProperties(&prop, cfg->device_id));
   ctx->numCU = prop.multiProcessorCount;
-  {
-    // the context's own stream (the running-mean updates' when the caller sets none) at the highest
-    // stream priority on request (PT_STREAM_PRIORITY=1; measured slower: an N = 8 share of c2
-    // 0.085 -> 0.124 ms per frame, c4 0.149 either way)
-    const char* e = std::getenv("PT_STREAM_PRIORITY");
-    int least = 0, greatest = 0;
-    if (e && std::atoi(e) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-      CKC(hipStreamCreateWithPriority(&ctx->own, hipStreamNonBlocking, greatest));
-    else
-      CKC(hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking));
-  }
+  CKC(hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking));
   ctx->stream = ctx->own;
   const size_t npix = (size_t)cfg->width * cfg->height;
   CKC(hipMalloc(&ctx->d_accum, npix * sizeof(float4)));
@@ -364,17 +344,20 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   const int owned = (numShards - cfg->tile_rank + cfg->tile_world - 1) / cfg->tile_world;
   ctx->numItems = owned * (ss / 8) * (ss / 8);
   ctx->perQueue = (ctx->numItems + NUM_QUEUES - 1) / NUM_QUEUES;
-  // the default megakernel pipelines its frames (not BASIC, the fetch counter, the
-  // wavefront / regeneration kernels or PT_FLAG_SERIAL_FRAMES)
-  if (const char* e = std::getenv("PT_REGEN_WIDE")) ctx->regenWide = std::atoi(e) != 0 ? 1 : 0;
+  // the default megakernel and the regen kernel pipeline their frames (not BASIC, the fetch
+  // counter, the wavefront pipeline or PT_FLAG_SERIAL_FRAMES)
   ctx->pipe = cfg->integrator != PT_BASIC_CPU_COMPAT &&
-              !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_WAVEFRONT | PT_FLAG_REGEN | PT_FLAG_SERIAL_FRAMES));
+              !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_WAVEFRONT | PT_FLAG_SERIAL_FRAMES));
   if (ctx->pipe) {
-    // a process has GPU_MAX_HW_QUEUES hardware queues (HIP's default 4; the Python package and
-    // bench.py ask for 12): streams beyond them share queues and serialise, so the slot streams,
-    // the context's own stream and the caller's (torch's) must fit
-    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
+    // a process has the hardware queues its HIP runtime was initialised with (GPU_MAX_HW_QUEUES,
+    // HIP's default 4; the Python package asks for 12 when it is unset and HIP not yet initialised,
+    // and passes what is in effect as pt_config.hw_queues): streams beyond them share queues and
+    // serialise, so the slot streams, the context's own stream and the caller's (torch's) must fit
+    int hwq = cfg->hw_queues;
+    if (hwq <= 0) {
+      const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+      hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
+    }
     ctx->pipeDepth = std::min(ctx->pipeDepth, std::max(2, hwq - 2));
     // Whole Lambert frames (the regen kernel on every scene): 6 in flight. c2's bench line (20 frames
     // from an idle GPU) 0.254-0.257 ms per frame at 6 vs 0.259-0.277 at 8 and 0.259 at 4, 100 frames
@@ -386,14 +369,8 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
       ctx->pipeDepthFixed = true;
     }
     ctx->pipeDepthBase = ctx->pipeDepth;
-    if (const char* e = std::getenv("PT_GRID_SHARE")) ctx->gridShare = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PT_GRID_PCT")) ctx->gridPct = std::min(800, std::max(10, std::atoi(e)));
-    if (const char* e = std::getenv("PT_SLOT_PRIORITY")) ctx->slotPriority = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PT_GRID_ALWAYS")) ctx->gridAlways = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PT_KERNEL_MIX")) ctx->kernelMix = std::atoi(e) != 0;
-    CKC(hipEventCreateWithFlags(&ctx->protoInit, hipEventDisableTiming));
-    CKC(hipEventCreateWithFlags(&ctx->callerMark, hipEventDisableTiming));
-    CKC(hipMalloc(&ctx->d_frameVars, PIPE * sizeof(FrameVar)));
+    ctx->batchCap = cfg->frame_batch > 0 ? std::min(cfg->frame_batch, MAX_BATCH)
+                                         : std::max(1, std::min(cfg->tile_world, MAX_BATCH));
     // slot streams are created as a depth first uses them (ensureSlots): streams beyond the
     // hardware queues share queues, which serialises their work
     for (int k = 0; k < COLS; k++) CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
@@ -462,7 +439,6 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
-  dfree(ctx->d_frameVars); dfree(ctx->d_tileDone); dfree(ctx->d_mixState);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
   freePrimaryBins(ctx->bins);
   for (int k = 0; k < PIPE; k++) {
@@ -503,46 +479,10 @@ static inline void nrm3(const float* a, const float* b, const float* c, float N[
 struct WideTree {
   std::vector<float4> bvh;
   int rootRef = REF_NONE, nDev = 0, depth = 0;
-  bool quant = false;  // 3-float4 quantized records (pt_trace.h visitNodeQ) instead of 4-float4 exact ones
 };
 
-// One axis of a quantized node: origin o and scale 2^k for the planes of both
-// children, then each plane rounded one step outward beyond its own rounding
-// (pt_trace.h visitNodeQ decodes origin + q * 2^k with one rounding of the add).
-static bool quantAxis(const float* lo, const float* hi, const bool* valid, float& o, int& kOut, uint8_t q[4]) {
-  float mn = INFINITY, mx = -INFINITY;
-  for (int c = 0; c < 2; c++)
-    if (valid[c]) { mn = std::min(mn, lo[c]); mx = std::max(mx, hi[c]); }
-  if (!(mn <= mx)) { o = 0.0f; kOut = 0; q[0] = q[1] = q[2] = q[3] = 0; return true; }
-  o = mn;
-  const double e = (double)mx - (double)mn;
-  const float mag = std::max(std::fabs(mn), std::fabs(mx));
-  int E = 0;
-  std::frexp(mag > 0.0f ? mag : 1e-30f, &E);  // mag in [2^(E-1), 2^E)
-  int k = (E - 1) - 23 + 2;                    // 2^k >= 4 ulp(mag)
-  if (e > 0.0) k = std::max(k, (int)std::ceil(std::log2(e / 250.0)));
-  k = std::max(k, -126);
-  if (k > 127) return false;
-  const double sc = std::ldexp(1.0, k);
-  const float sf = (float)sc;
-  for (int c = 0; c < 2; c++) {
-    uint8_t* ql = &q[2 * c];
-    if (!valid[c]) { ql[0] = ql[1] = 0; continue; }
-    long a = (long)std::floor(((double)lo[c] - o) / sc) - 1, b = (long)std::ceil(((double)hi[c] - o) / sc) + 1;
-    a = std::max(0L, a);
-    b = std::min(255L, b);
-    // the device's decode, checked: a plane may only move outward
-    while (a > 0 && !(o + (float)a * sf <= lo[c])) a--;
-    while (b < 255 && !(o + (float)b * sf >= hi[c])) b++;
-    if (!(o + (float)a * sf <= lo[c]) || !(o + (float)b * sf >= hi[c])) return false;
-    ql[0] = (uint8_t)a;
-    ql[1] = (uint8_t)b;
-  }
-  kOut = k;
-  return true;
-}
 static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, float inflate, WideTree& out,
-                                  float inflateAbs = 0.0f, bool quantize = false) {
+                                  float inflateAbs = 0.0f) {
   auto nodeN = [&](int k) { return (int)nodes[(size_t)k * 12 + 3]; };
   auto isInternal = [&](int k) { return k > 0 && k < nNodes && nodeN(k) <= 0; };
   // depth of the reachable tree (bounds the traversal stack; rejects cycles)
@@ -607,9 +547,7 @@ static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, floa
     hi.x += e[0]; hi.y += e[1]; hi.z += e[2];
   };
   std::vector<float4>& bvh = out.bvh;
-  const int F4 = quantize ? 3 : 4;
-  out.quant = quantize;
-  bvh.assign(std::max<size_t>(order.size(), 1) * F4, make_float4(0, 0, 0, 0));
+  bvh.assign(std::max<size_t>(order.size(), 1) * 4, make_float4(0, 0, 0, 0));
   const float inf = INFINITY;
   for (size_t id = 0; id < order.size(); id++) {
     const int k = order[id];
@@ -632,32 +570,6 @@ static std::string encodeWideTree(const float* nodes, int nNodes, int nTri, floa
     float refs[2];
     std::memcpy(&refs[0], &lr, 4);
     std::memcpy(&refs[1], &rr, 4);
-    if (quantize) {
-      const bool valid[2] = {lr != REF_NONE, rr != REF_NONE};
-      const float los[3][2] = {{la.x, ra.x}, {la.y, ra.y}, {la.z, ra.z}};
-      const float his[3][2] = {{lb.x, rb.x}, {lb.y, rb.y}, {lb.z, rb.z}};
-      float o[3];
-      int k[3];
-      uint8_t q[3][4];  // per axis: L.lo, L.hi, R.lo, R.hi
-      for (int a = 0; a < 3; a++)
-        if (!quantAxis(los[a], his[a], valid, o[a], k[a], q[a])) return "quantize";
-      // plane bytes L.lo.xyz L.hi.xyz R.lo.xyz R.hi.xyz, then the left ref
-      const uint8_t b[12] = {q[0][0], q[1][0], q[2][0], q[0][1], q[1][1], q[2][1],
-                             q[0][2], q[1][2], q[2][2], q[0][3], q[1][3], q[2][3]};
-      uint32_t w[3], ebits = 0;
-      std::memcpy(w, b, 12);
-      for (int a = 0; a < 3; a++) ebits |= (uint32_t)(k[a] + 127) << (8 * a);
-      float fw[4];
-      std::memcpy(&fw[0], &w[0], 4);
-      std::memcpy(&fw[1], &w[1], 4);
-      std::memcpy(&fw[2], &w[2], 4);
-      float fe;
-      std::memcpy(&fe, &ebits, 4);
-      bvh[3 * id + 0] = make_float4(o[0], o[1], o[2], fe);
-      bvh[3 * id + 1] = make_float4(fw[0], fw[1], fw[2], refs[0]);
-      bvh[3 * id + 2] = make_float4(refs[1], 0.0f, 0.0f, 0.0f);
-      continue;
-    }
     bvh[4 * id + 0] = make_float4(la.x, ra.x, la.y, ra.y);
     bvh[4 * id + 1] = make_float4(la.z, ra.z, lb.x, rb.x);
     bvh[4 * id + 2] = make_float4(lb.y, rb.y, lb.z, rb.z);
@@ -876,9 +788,8 @@ static void prepareAccel(const float* tris, int nTri, const float* nodes, int nN
       h.leafBox[2 * (size_t)i + 1] = h.refBox[2 * (size_t)leafOf[i] + 1];
     }
   }
-  // the tree itself: on the GPU by uploadScene (pt_build.hip), or here (scene.cpp's threaded
-  // binned SAH; the quantized record kind is encoded on the host only)
-  if (!hostBuild && !FAST_QUANT) {
+  // the tree itself: on the GPU by uploadScene (pt_build.hip), or here (scene.cpp's threaded binned SAH)
+  if (!hostBuild) {
     h.deviceBuild = true;
     h.fast = true;
     return;
@@ -895,10 +806,7 @@ static void prepareAccel(const float* tris, int nTri, const float* nodes, int nN
   float sceneScale = 0.0f;
   for (int i = 0; i < nTri; i++)
     for (int k = 0; k < 9; k++) sceneScale = std::max(sceneScale, std::fabs(tris[(size_t)i * 36 + k]));
-  // (a tree whose planes do not quantize is not used: the traversal's record kind is FAST_QUANT)
-  if (!encodeWideTree(an.data(), (int)(an.size() / 12), nTri, 1e-5f, h.fastTree, 3e-5f * sceneScale, FAST_QUANT)
-           .empty())
-    return;
+  if (!encodeWideTree(an.data(), (int)(an.size() / 12), nTri, 1e-5f, h.fastTree, 3e-5f * sceneScale).empty()) return;
   buildPairs(h.geo, h.order.data(), nTri, h.fpairs);
   h.accelMs = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h.fast = true;
@@ -960,6 +868,7 @@ static std::string prepareScene(const float* tris, int nTri, const float* nodes,
 }
 
 static int syncStreams(pt_ctx* ctx);
+static int ensureBasicImage(pt_ctx* ctx);
 
 static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   if (int rc = syncStreams(ctx)) return rc;  // no frame in flight reads the buffers replaced here
@@ -1049,14 +958,6 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
     std::vector<float4> w4;
     encodeWide4(an.data(), nn, h.nTri, 1e-5f, 3e-5f * scale, w4, ctx->f4Root, ctx->f4nDev, ctx->f4Depth);
     if ((rc = upload(ctx, &ctx->d_fbvh4, w4))) return rc;
-  }
-  if (PT_W4_HALF) {  // the traversals' records: child planes as halves rounded outward (halfNodes4Kernel)
-    float4* hn = nullptr;
-    CK(hipMalloc(&hn, (size_t)std::max(ctx->f4nDev, 1) * W4_NODE_F4 * sizeof(float4)));
-    CK(launchHalfNodes4(ctx->d_fbvh4, ctx->f4nDev, hn, ctx->stream));
-    CK(hipStreamSynchronize(ctx->stream));
-    dfree(ctx->d_fbvh4);
-    ctx->d_fbvh4 = hn;
   }
   ctx->fast4Ready = true;
   // a visit pushes up to three children: the traversal stack needs 3 entries per wide level
@@ -1324,8 +1225,9 @@ static int launchEvents(pt_ctx* ctx, hipEvent_t* b, hipEvent_t* e) {
   return PT_OK;
 }
 
-// the launch whose events launchEvents handed out has been enqueued
-static void commitLaunch(pt_ctx* ctx) {
+// the launch whose events launchEvents handed out has been enqueued (it renders `frames` frames)
+static void commitLaunch(pt_ctx* ctx, int frames = 1) {
+  ctx->frames += frames;
   const int k = (int)(ctx->issued % EV_RING);
   ctx->evProbe[k] = ctx->tagSlot;
   ctx->evGen[k] = ctx->probeGen;
@@ -1360,7 +1262,7 @@ static SceneView sceneView(const pt_ctx* ctx) {
   s.fnTop = std::min(LDS_NODES, ctx->fnDev);
   s.fbvh4 = ctx->d_fbvh4;
   s.f4Root = ctx->f4Root;
-  s.f4nTop = std::min(LDS_NODES * 4 / W4_NODE_F4, ctx->f4nDev);  // the LDS copy holds LDS_NODES * 4 float4
+  s.f4nTop = std::min(LDS_NODES * 4 / W4_F4, ctx->f4nDev);  // the LDS copy holds LDS_NODES * 4 float4
   s.refLeafOf = ctx->d_refLeafOf;
   s.refParent = ctx->d_refParent;
   s.refBox = ctx->d_refBox;
@@ -1596,22 +1498,19 @@ static PackParams packParams(const pt_ctx* ctx, int rank, int world);
 // the slot streams (and their events) of depth D
 static int ensureSlots(pt_ctx* ctx, int D) {
   for (int k = 0; k < D; k++) {
-    if (!ctx->slotStream[k]) {
-      // the frames' streams at the lowest priority: the running-mean updates (on the caller's
-      // stream) and the caller's own work get the CUs first as the frames' waves retire
-      int least = 0, greatest = 0;
-      if (ctx->slotPriority && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-        CK(hipStreamCreateWithPriority(&ctx->slotStream[k], hipStreamNonBlocking, least));
-      else
-        CK(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
-    }
+    if (!ctx->slotStream[k]) CK(hipStreamCreateWithFlags(&ctx->slotStream[k], hipStreamNonBlocking));
     if (!ctx->kernelDone[k]) CK(hipEventCreateWithFlags(&ctx->kernelDone[k], hipEventDisableTiming));
   }
   return PT_OK;
 }
 
-static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
+// One launch: frame frameCounter, or -- pipelined, with no policy probe running and the batch
+// not starting a running mean -- up to `want` consecutive frames of the same camera
+// (RenderParams::nFrames, at most ctx->batchCap). *done = the frames rendered.
+static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter,
+                     int want = 1, int* done = nullptr) {
   if (!ctx) return PT_E_INVALID;
+  if (done) *done = 1;
   CK(hipSetDevice(ctx->cfg.device_id));
   const pt_config& c = ctx->cfg;
   unsigned long long* stats = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_STATS);
@@ -1620,11 +1519,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     if (!ctx->d_shapes) return fail(ctx, PT_E_NOSCENE, "no BASIC shapes uploaded");
     const int maxDepth = c.max_bounce >= 0 ? c.max_bounce : 8;  // B:254
     if (maxDepth > BASIC_MAX_DEPTH) return fail(ctx, PT_E_INVALID, "BASIC max_bounce > 31");
-    const size_t npix = (size_t)c.width * c.height;
-    if (!ctx->d_basicImg) {
-      CK(hipMalloc(&ctx->d_basicImg, npix * 3 * sizeof(double)));
-      CK(hipMemsetAsync(ctx->d_basicImg, 0, npix * 3 * sizeof(double), ctx->stream));
-    }
+    if (int rc = ensureBasicImage(ctx)) return rc;
     if (!ctx->d_overruns) {
       CK(hipMalloc(&ctx->d_overruns, sizeof(unsigned long long)));
       CK(hipMemsetAsync(ctx->d_overruns, 0, sizeof(unsigned long long), ctx->stream));
@@ -1682,8 +1577,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   }
   const int D = piped ? ctx->pipeDepth : 1;
   const int slot = piped ? (int)(ctx->frameNo % (unsigned)D) : 0;
-  const bool protoFrame = piped && D > 1 && ctx->kernelMix && !regen;  // the in-kernel running mean (below)
-  const int nCol = protoFrame ? D + 1 : 2 * D + 1;
+  const int nCol = 2 * D + 1;
   const int colIdx = piped ? (int)(ctx->frameNo % (unsigned)nCol) : 0;
   hipStream_t S = piped ? ctx->slotStream[slot] : ctx->stream;
   // every other slot's frame in flight has ended on S (the frames that read buffers
@@ -1711,20 +1605,24 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // A caller that waits for every frame gets the whole machine for each.
   const int fullGrid = ctx->numCU * nb;
   int grid = fullGrid;
-  if (piped && D > 1 && ctx->gridShare) {
-    bool others = ctx->gridAlways;  // another frame still in flight: the caller streams frames
+  // While other frames are in flight, each frame's grid is 150 % of its equal share: a frame
+  // finishing early leaves waves of the others ready to take its place (measured against 100 /
+  // 200 / 300 % with the bench line as the driver runs it, 20 frames from an idle GPU: c2 0.285 /
+  // 0.262 / 0.266 / 0.289 ms per frame at 100 / 150 / 200 / 300, c4 0.413 / 0.360 / 0.367 / 0.385)
+  constexpr int GRID_PCT = 150;
+  if (piped && D > 1) {
+    bool others = false;  // another frame still in flight: the caller streams frames
     for (int k = 0; k < D && !others; k++)
       others = k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
     (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
-    if (others) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * ctx->gridPct / (100 * D)));
+    if (others) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * D)));
   }
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)fullGrid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
   if (rc) return rc;
   const size_t npix = (size_t)c.width * c.height;
-  if (piped && !ctx->d_col[colIdx]) CK(hipMalloc(&ctx->d_col[colIdx], npix * sizeof(float4)));
-  // the colour buffer's previous frame (nCol back) has been mixed (the slot's queue counters,
-  // order list and camera-ray results belong to its previous frame on this same stream)
+  // the colour buffer's previous launch (nCol back) has been mixed (the slot's queue counters,
+  // order list and camera-ray results belong to its previous launch on this same stream)
   if (piped && ctx->frameNo >= (unsigned long long)nCol) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
   int* queue = reinterpret_cast<int*>(ctx->d_ctl + CTL_QUEUES) + (size_t)slot * NUM_QUEUES * CTL_LINE_INTS;
   RenderParams p;
@@ -1743,7 +1641,6 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   std::memcpy(p.eye, eye, sizeof(p.eye));
   std::memcpy(p.cam, cameraRotate, sizeof(p.cam));
   p.accum = ctx->d_accum;
-  p.col = piped ? ctx->d_col[colIdx] : nullptr;
   p.queue = queue;
   p.perQueue = ctx->perQueue;
   p.numItems = ctx->numItems;
@@ -1788,6 +1685,25 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (regen && wide) p.scene.f4nTop = std::min(regenTop4(c.integrator), ctx->f4nDev);  // its own LDS copy's size
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
+  // While the policy probe times frames (PT_SPLIT_AUTO, 20 frames after a restart) a pipelined
+  // frame starts only after the previous one has ended, and each launch is one frame.
+  const bool probing = ordered && PT_SPLIT_AUTO &&
+                       (ctx->treeDecided < 0 || ctx->splitDecided < 0 || ctx->orderDecided < 0);
+  const int nF = piped && !probing ? std::max(1, std::min(want, ctx->batchCap)) : 1;
+  if (done) *done = nF;
+  p.nFrames = nF;
+  p.sampleStride = c.sample_world > 0 ? (uint32_t)c.sample_world : 1u;
+  p.colStride = npix;
+  if (piped && ctx->colCap[colIdx] < nF) {  // room for the launch's frames (each buffer grows once, to batchCap)
+    if (ctx->d_col[colIdx]) {
+      CK(hipEventSynchronize(ctx->mixDone[colIdx]));  // its last frames' running-mean update has read it
+      dfree(ctx->d_col[colIdx]);
+    }
+    const int cap = std::max(nF, ctx->batchCap);
+    CK(hipMalloc(&ctx->d_col[colIdx], (size_t)cap * npix * sizeof(float4)));
+    ctx->colCap[colIdx] = cap;
+  }
+  p.col = piped ? ctx->d_col[colIdx] : nullptr;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
   // camera-ray bins, rebuilt when the camera or the scene changed (the previous frame
   // has ended first: it may still read the old bins); they need the reference facts
@@ -1826,7 +1742,15 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     p.binTilesX = ctx->bins.tilesX;
     p.binTilesY = ctx->bins.tilesY;
     if (pass) {
-      if (!ctx->d_prim[slot]) CK(hipMalloc(&ctx->d_prim[slot], npix * sizeof(int2)));
+      if (ctx->primCap[slot] < nF) {  // the slot's previous launch (on S) may still read the old results
+        if (ctx->d_prim[slot]) {
+          CK(hipStreamSynchronize(S));
+          dfree(ctx->d_prim[slot]);
+        }
+        const int cap = std::max(nF, piped ? ctx->batchCap : 1);
+        CK(hipMalloc(&ctx->d_prim[slot], (size_t)cap * npix * sizeof(int2)));
+        ctx->primCap[slot] = cap;
+      }
       p.primHit = ctx->d_prim[slot];
     }
   }
@@ -1837,53 +1761,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.orderCap = orderCap;
   p.tileCost = orderedNow ? cost : nullptr;
   p.tileCostMax = orderedNow ? cost + ctx->numItems : nullptr;
-  if (!orderedNow && !regen && !count && PT_STATIC_PCT > 0) {
-    p.staticItems = (int)((long long)ctx->numItems * PT_STATIC_PCT / 100);
-    p.dynPerQueue = (ctx->numItems - p.staticItems + NUM_QUEUES - 1) / NUM_QUEUES;
-  }
-  // While the policy probe times frames (PT_SPLIT_AUTO, 20 frames after a restart)
-  // a pipelined frame still starts only after the previous one has ended.
-  const bool probing = ordered && PT_SPLIT_AUTO &&
-                       (ctx->treeDecided < 0 || ctx->splitDecided < 0 || ctx->orderDecided < 0);
   if (piped && probing) {
     if (int e = waitOthers()) return e;
-  }
-  // The running mean inside the frame kernels (completeItem): every pipelined megakernel
-  // frame, once the tile protocol's state is valid for it -- else, first, after every
-  // earlier frame and the caller's stream's work so far (a cleared accumulation), the
-  // state is reset on this frame's stream and every slot's next frame waits for that.
-  const bool proto = protoFrame;
-  if (proto) {
-    if (!ctx->d_tileDone) {
-      CK(hipMalloc(&ctx->d_tileDone, (size_t)COLS * ctx->numItems * sizeof(int)));
-      CK(hipMalloc(&ctx->d_mixState, (size_t)ctx->numItems * sizeof(unsigned)));
-    }
-    if (!ctx->protoValid || ctx->protoNext != ctx->frameNo) {
-      CK(hipEventRecord(ctx->callerMark, ctx->stream));
-      CK(hipStreamWaitEvent(S, ctx->callerMark, 0));
-      for (int k = 0; k < D; k++)
-        if (k != slot && ctx->slotBusy[k]) CK(hipStreamWaitEvent(S, ctx->kernelDone[k], 0));
-      if (ctx->mixPending) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastCol], 0));
-      CK(hipMemsetAsync(ctx->d_tileDone, 0, (size_t)COLS * ctx->numItems * sizeof(int), S));
-      CK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->d_mixState), (int)(2u * (uint32_t)ctx->frameNo),
-                           (size_t)ctx->numItems, S));
-      CK(hipEventRecord(ctx->protoInit, S));
-      ctx->protoGen++;
-      ctx->protoGenSeen[slot] = ctx->protoGen;
-      ctx->protoValid = true;
-    }
-    if (ctx->protoGenSeen[slot] != ctx->protoGen) {
-      CK(hipStreamWaitEvent(S, ctx->protoInit, 0));
-      ctx->protoGenSeen[slot] = ctx->protoGen;
-    }
-    ctx->protoNext = ctx->frameNo + 1;
-    p.tileDone = ctx->d_tileDone;
-    p.mixState = ctx->d_mixState;
-    p.frameVars = ctx->d_frameVars;
-    p.seq = (uint32_t)ctx->frameNo;
-    p.depth = D;
-  } else if (piped) {
-    ctx->protoValid = false;  // this frame's running mean is mixKernel's
   }
   int erc = launchEvents(ctx, &evb, &eve);
   if (erc) return erc;
@@ -1899,19 +1778,11 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   }
   p.waveTrace = dTrace;
 #endif
-  // the slot's work-queue counters zeroed for this frame: by the camera-ray pass (block 0), by
-  // frameVarKernel for the in-kernel running mean's frames, else by a memset
+  // the slot's work-queue counters zeroed for this launch: by the camera-ray pass (block 0), else by a memset
   p.zeroQueue = p.primHit != nullptr;
-  if (!p.primHit && !proto) CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
+  if (!p.primHit) CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   CK(hipEventRecord(evb, S));
   if (p.primHit) CK(launchPrimary(p, S));
-  if (proto) {  // its FrameVar for the earlier frames' waves that may mix its tiles; its queue counters zeroed
-    FrameVar fv;
-    fv.col = p.col;
-    fv.sampleIndex = p.sampleIndex;
-    fv.frameCounter = p.frameCounter;
-    CK(launchFrameVar(fv, ctx->d_frameVars + slot, queue, S));
-  }
   if (regen) CK(launchRegen(p, c.integrator, grid, S, cull, wide));
   else CK(launchRender(p, c.integrator, grid, S, cull, count, wide));
 #if PT_WAVE_TRACE
@@ -1936,42 +1807,23 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // kernel_ms: the frame's own kernels (camera-ray pass, frame kernel, reorder), so the
   // policy probe weighs the order's cost too; the running-mean update below is not in it
   CK(hipEventRecord(eve, S));
-  if (proto) {
-    // A tile's mix of frame g runs in a kernel up to g's own, so the frame is mixed in once
-    // every kernel up to its own has ended: its end waits for the previous frame's end (by
-    // induction, every earlier frame's). The caller's stream follows it (whatever the caller
-    // queues behind the frame sees its update).
-    if (ctx->frameNo >= 1) {
-      const int prev = (int)((ctx->frameNo - 1) % (unsigned)D);
-      if (ctx->slotBusy[prev]) CK(hipStreamWaitEvent(S, ctx->kernelDone[prev], 0));
-    }
-    // follows it (whatever the caller queues behind the frame sees its update)
-    CK(hipEventRecord(ctx->kernelDone[slot], S));
-    ctx->slotBusy[slot] = true;
-    CK(hipEventRecord(ctx->mixDone[colIdx], S));
-    CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[colIdx], 0));
-    ctx->lastMixStream = ctx->stream;
-    ctx->lastSlot = slot;
-    ctx->lastCol = colIdx;
-    ctx->mixPending = true;
-    ctx->frameNo++;
-  } else if (piped) {
-    // the running-mean update on the caller's stream, in frame order, after this frame's kernel
+  if (piped) {
+    // the running-mean updates on the caller's stream, in frame order, after this launch's kernel
     CK(hipEventRecord(ctx->kernelDone[slot], S));
     ctx->slotBusy[slot] = true;
     CK(hipStreamWaitEvent(ctx->stream, ctx->kernelDone[slot], 0));
     if (ctx->mixPending && ctx->lastMixStream != ctx->stream)  // the caller switched streams: keep frame order
       CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastCol], 0));
     ctx->lastMixStream = ctx->stream;
-    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[colIdx], frameCounter,
-                 ctx->stream));
+    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[colIdx], npix, nF,
+                 frameCounter, ctx->stream));
     CK(hipEventRecord(ctx->mixDone[colIdx], ctx->stream));
     ctx->lastSlot = slot;
     ctx->lastCol = colIdx;
     ctx->mixPending = true;
     ctx->frameNo++;
   }
-  commitLaunch(ctx);
+  commitLaunch(ctx, nF);
   return PT_OK;
 }
 
@@ -1998,12 +1850,27 @@ static int syncStreams(pt_ctx* ctx) {
 static int groupGather(pt_ctx* ctx);
 
 int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter) {
-  if (!ctx) return PT_E_INVALID;
-  if (ctx->peers.empty()) return renderOne(ctx, eye, cameraRotate, frameCounter);
-  // every device renders its tiles on its own stream; then the gather (GroupGather)
-  for (pt_ctx* m : members(ctx))
-    if (int rc = renderOne(m, eye, cameraRotate, frameCounter)) return fromPeer(ctx, m, rc);
-  return groupGather(ctx);
+  return pt_render_frames_async(ctx, eye, cameraRotate, frameCounter, 1);
+}
+
+int pt_render_frames_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter,
+                           int nFrames) {
+  if (!ctx || nFrames < 0) return PT_E_INVALID;
+  while (nFrames > 0) {
+    int done = 1;
+    if (ctx->peers.empty()) {
+      if (int rc = renderOne(ctx, eye, cameraRotate, frameCounter, nFrames, &done)) return rc;
+    } else {
+      // a device group: every device renders its tiles of the frame on its own stream; then the
+      // gather (GroupGather), frame by frame
+      for (pt_ctx* m : members(ctx))
+        if (int rc = renderOne(m, eye, cameraRotate, frameCounter)) return fromPeer(ctx, m, rc);
+      if (int rc = groupGather(ctx)) return rc;
+    }
+    frameCounter += (uint32_t)done;
+    nFrames -= done;
+  }
+  return PT_OK;
 }
 
 int pt_render_frame(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter,
@@ -2071,11 +1938,36 @@ int pt_download_accum(pt_ctx* ctx, float* accum) {
   return PT_OK;
 }
 
+// the BASIC double image (basicKernel adds each sample to it), allocated and zeroed on first use
+static int ensureBasicImage(pt_ctx* ctx) {
+  if (ctx->d_basicImg) return PT_OK;
+  const size_t n = (size_t)ctx->cfg.width * ctx->cfg.height * 3;
+  CK(hipMalloc(&ctx->d_basicImg, n * sizeof(double)));
+  CK(hipMemsetAsync(ctx->d_basicImg, 0, n * sizeof(double), ctx->stream));
+  return PT_OK;
+}
+
 static int uploadAccumOne(pt_ctx* ctx, const float* accum) {
   if (int rc = joinPipe(ctx)) return rc;
   CK(hipSetDevice(ctx->cfg.device_id));
-  const size_t bytes = (size_t)ctx->cfg.width * ctx->cfg.height * sizeof(float4);
-  CK(hipMemcpyAsync(ctx->d_accum, accum, bytes, hipMemcpyDefault, ctx->stream));  // host or device
+  const size_t npix = (size_t)ctx->cfg.width * ctx->cfg.height;
+  CK(hipMemcpyAsync(ctx->d_accum, accum, npix * sizeof(float4), hipMemcpyDefault, ctx->stream));  // host or device
+  if (ctx->cfg.integrator == PT_BASIC_CPU_COMPAT) {  // basicKernel continues from its double image: the sums, widened
+    if (int rc = ensureBasicImage(ctx)) return rc;
+    CK(launchBasicWiden(ctx->d_accum, ctx->d_basicImg, (long)npix, ctx->stream));
+  }
+  CK(hipStreamSynchronize(ctx->stream));
+  return PT_OK;
+}
+
+int pt_upload_basic_image(pt_ctx* ctx, const double* rgb) {
+  if (!ctx || !rgb) return PT_E_INVALID;
+  if (ctx->cfg.integrator != PT_BASIC_CPU_COMPAT) return fail(ctx, PT_E_INVALID, "not a BASIC context");
+  if (int rc = syncStreams(ctx)) return rc;
+  if (int rc = ensureBasicImage(ctx)) return rc;
+  const size_t npix = (size_t)ctx->cfg.width * ctx->cfg.height;
+  CK(hipMemcpyAsync(ctx->d_basicImg, rgb, npix * 3 * sizeof(double), hipMemcpyDefault, ctx->stream));
+  CK(launchBasicNarrow(ctx->d_basicImg, ctx->d_accum, (long)npix, ctx->stream));  // the f32 sums, as a frame leaves them
   CK(hipStreamSynchronize(ctx->stream));
   return PT_OK;
 }
@@ -2094,7 +1986,6 @@ int pt_clear_accum(pt_ctx* ctx) {
   if (int rc = joinGather(ctx)) return rc;
   for (pt_ctx* m : members(ctx)) {
     if (int rc = joinPipe(m)) return fromPeer(ctx, m, rc);
-    m->protoValid = false;  // the next frame's kernel updates the accumulation after this clear
     if (hipSetDevice(m->cfg.device_id) != hipSuccess ||
         hipMemsetAsync(m->d_accum, 0, (size_t)m->cfg.width * m->cfg.height * sizeof(float4), m->stream) != hipSuccess)
       return fail(ctx, PT_E_HIP, "pt_clear_accum on device " + std::to_string(m->cfg.device_id));
@@ -2282,6 +2173,8 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->kernel_ms = ctx->launches > 0 ? ctx->msLast : 0.0f;
   st->kernel_ms_total = (float)ctx->msTotal;
   st->launches = ctx->launches;
+  st->frames = ctx->frames;
+  st->frame_batch = ctx->batchCap;
   st->max_stack = ctx->maxStack;
   st->split_items = 0;
   st->runtime_tree = ctx->lastFast ? 1 : 0;
@@ -2361,6 +2254,7 @@ static int resetOne(pt_ctx* ctx) {
   while (foldOne(ctx, true)) {
   }
   ctx->launches = 0;
+  ctx->frames = 0;
   ctx->msTotal = 0.0;
   ctx->msLast = 0.0f;
   return PT_OK;

@@ -101,31 +101,6 @@ __device__ __forceinline__ void visitNode(const float4* nd, V3 o, V3 inv, NodeHi
   h.lref = __float_as_int(q3.x);
   h.rref = __float_as_int(q3.y);
 }
-// The runtime tree's quantized node (pt_runtime.cpp encodeWideTree, 36 of its
-// 48 bytes read): {origin.xyz, per-axis scale exponents}, 12 plane bytes
-// (L.lo.xyz L.hi.xyz R.lo.xyz R.hi.xyz) + left ref, {right ref}. A plane is
-// origin + q * 2^k: the multiply is exact, the add rounds once, and the host
-// rounded every plane one step outward beyond that, so the decoded boxes
-// contain the exact ones (whose results refReachable checks anyway).
-__device__ __forceinline__ float qscale(uint32_t bits, int axis) {
-  return __uint_as_float(((bits >> (8 * axis)) & 255u) << 23);  // 2^(byte - 127)
-}
-__device__ __forceinline__ void visitNodeQ(const float4* nd, V3 o, V3 inv, NodeHit& h) {
-  const float4 c0 = nd[0], c1 = nd[1];
-  const float c2 = nd[2].x;
-  const uint32_t e = __float_as_uint(c0.w);
-  const f32x2 sx = {qscale(e, 0), qscale(e, 0)}, sy = {qscale(e, 1), qscale(e, 1)}, sz = {qscale(e, 2), qscale(e, 2)};
-  const f32x2 Ox = {c0.x, c0.x}, Oy = {c0.y, c0.y}, Oz = {c0.z, c0.z};
-  const uint32_t w0 = __float_as_uint(c1.x), w1 = __float_as_uint(c1.y), w2 = __float_as_uint(c1.z);
-  auto b = [](uint32_t w, int k) { return (float)((w >> (8 * k)) & 255u); };
-  const f32x2 lox = Ox + f32x2{b(w0, 0), b(w1, 2)} * sx, loy = Oy + f32x2{b(w0, 1), b(w1, 3)} * sy,
-              loz = Oz + f32x2{b(w0, 2), b(w2, 0)} * sz;
-  const f32x2 hix = Ox + f32x2{b(w0, 3), b(w2, 1)} * sx, hiy = Oy + f32x2{b(w1, 0), b(w2, 2)} * sy,
-              hiz = Oz + f32x2{b(w1, 1), b(w2, 3)} * sz;
-  slabPair(lox, loy, loz, hix, hiy, hiz, o, inv, h);
-  h.lref = __float_as_int(c1.w);
-  h.rref = __float_as_int(c2);
-}
 // The runtime tree's slab tests fused: (plane - o) * inv as fma(plane, inv,
 // -o * inv), one packed FMA per axis and child pair instead of a subtract and a
 // multiply. The rounding differs from hitAABB's by about |o| * 2^-23 along each
@@ -172,19 +147,15 @@ __device__ __forceinline__ FusedRay fusedRay(V3 o, V3 inv) {
   return f;
 }
 // Node kinds, a compile-time property of a traversal: the reference tree's
-// exact records and slab tests (NODE_EXACT), the runtime tree's quantized
-// records (NODE_QUANT, PT_QUANT_NODES) or its exact records with fused slab
-// tests (NODE_FUSED).
-constexpr int NODE_EXACT = 0, NODE_QUANT = 1, NODE_FUSED = 2;
-constexpr int FAST_KIND = FAST_QUANT ? NODE_QUANT : (PT_FUSED_SLABS ? NODE_FUSED : NODE_EXACT);
+// exact records and slab tests (NODE_EXACT) or the runtime tree's records with
+// fused slab tests (NODE_FUSED).
+constexpr int NODE_EXACT = 0, NODE_FUSED = 2;
+constexpr int FAST_KIND = PT_FUSED_SLABS ? NODE_FUSED : NODE_EXACT;
 template <int KIND>
 __device__ __forceinline__ void visitAny(const float4* nd, V3 o, V3 inv, const FusedRay& fr, NodeHit& h) {
-  if (KIND == NODE_QUANT) visitNodeQ(nd, o, inv, h);
-  else if (KIND == NODE_FUSED) visitNodeF(nd, fr.inv, fr.noi, h);
+  if (KIND == NODE_FUSED) visitNodeF(nd, fr.inv, fr.noi, h);
   else visitNode(nd, o, inv, h);
 }
-template <int KIND>
-constexpr int nodeF4() { return KIND == NODE_QUANT ? 3 : 4; }
 
 // hitTriangle IS:251-301, accept/reject and distance only. With the stored unit
 // normal Ng = normalize(cross(p2-p1,p3-p1)) and w = dot(Ng,p1) (computed on the
@@ -294,8 +265,8 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
         if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
       }
       NodeHit nh;
-      const float4* nd = S.bvh + (size_t)nodeF4<KIND>() * ref;
-      if (LDSTOP && ref < S.nTop) nd = top + nodeF4<KIND>() * ref;
+      const float4* nd = S.bvh + (size_t)4 * ref;
+      if (LDSTOP && ref < S.nTop) nd = top + 4 * ref;
       visitAny<KIND>(nd, o, inv, fr, nh);
       const int lref = nh.lref, rref = nh.rref;
       const float d1 = nh.d1, d2 = nh.d2, t0l = nh.t0l, t0r = nh.t0r;
@@ -402,29 +373,9 @@ __device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
   ra = r;
 }
 // one 4-wide record: child planes lo/hi per axis (children 0..3 in x..w) and the refs
-__device__ __forceinline__ float2 halves2(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return make_float2((float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu)),
-                     (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)));
-}
-__device__ __forceinline__ float4 halves4(float a, float b) {
-  const float2 p = halves2(a), q = halves2(b);
-  return make_float4(p.x, p.y, q.x, q.y);
-}
 __device__ __forceinline__ void loadNode4(const float4* nd, float4& lx, float4& ly, float4& lz, float4& hx, float4& hy,
                                           float4& hz, float4& rf) {
-#if PT_W4_HALF
-  const float4 a = nd[0], b = nd[1], c = nd[2];
-  rf = nd[3];
-  lx = halves4(a.x, a.y);
-  ly = halves4(a.z, a.w);
-  lz = halves4(b.x, b.y);
-  hx = halves4(b.z, b.w);
-  hy = halves4(c.x, c.y);
-  hz = halves4(c.z, c.w);
-#else
   lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
-#endif
 }
 template <bool CULL, class StackType, bool LDSTOP>
 __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
@@ -445,8 +396,8 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
         C.nodes++;
         if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) C.mats++;
       }
-      const float4* nd = S.fbvh4 + (size_t)W4_NODE_F4 * ref;
-      if (LDSTOP && ref < S.f4nTop) nd = top + W4_NODE_F4 * ref;
+      const float4* nd = S.fbvh4 + (size_t)W4_F4 * ref;
+      if (LDSTOP && ref < S.f4nTop) nd = top + W4_F4 * ref;
       float4 lx, ly, lz, hx, hy, hz, rf;
       loadNode4(nd, lx, ly, lz, hx, hy, hz, rf);
       float key[4];
@@ -565,16 +516,13 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
   const FusedRay fr = fusedRay(o, inv);
   const f32x2 ix = {fr.inv.x, fr.inv.x}, iy = {fr.inv.y, fr.inv.y}, iz = {fr.inv.z, fr.inv.z};
   const f32x2 ox = {fr.noi.x, fr.noi.x}, oy = {fr.noi.y, fr.noi.y}, oz = {fr.noi.z, fr.noi.z};
-#if PT_REGEN_YIELD_REL
-  yield = (__popcll(__ballot(true)) * yield + 63) >> 6;  // yield/64 of the lanes walking with this one
-#endif
   while (true) {
     const bool done = walk4Done(w);
     if (__ballot(!done) == 0 || __popcll(__ballot(done)) >= yield) break;  // wave-uniform
     if (done) continue;
     while (w.ref >= 0) {
-      const float4* nd = S.fbvh4 + (size_t)W4_NODE_F4 * w.ref;
-      if (LDSTOP && w.ref < S.f4nTop) nd = top + W4_NODE_F4 * w.ref;
+      const float4* nd = S.fbvh4 + (size_t)W4_F4 * w.ref;
+      if (LDSTOP && w.ref < S.f4nTop) nd = top + W4_F4 * w.ref;
       float4 lx, ly, lz, hx, hy, hz, rf;
       loadNode4(nd, lx, ly, lz, hx, hy, hz, rf);
       float key[4];
@@ -733,8 +681,8 @@ __device__ __forceinline__ int tracePacket(const SceneView& S, V3 o, V3 d, bool 
   while (true) {
     if (ref >= 0) {  // internal node: one scalar record for the wave
       NodeHit nh;
-      if (top && ref < S.nTop) visitAny<KIND>(top + nodeF4<KIND>() * ref, o, inv, fr, nh);  // LDS broadcast
-      else visitAny<KIND>(S.bvh + (size_t)nodeF4<KIND>() * ref, o, inv, fr, nh);
+      if (top && ref < S.nTop) visitAny<KIND>(top + 4 * ref, o, inv, fr, nh);  // LDS broadcast
+      else visitAny<KIND>(S.bvh + (size_t)4 * ref, o, inv, fr, nh);
       nh.lref = __builtin_amdgcn_readfirstlane(nh.lref);
       nh.rref = __builtin_amdgcn_readfirstlane(nh.rref);
       const bool active = (mask >> lane) & 1ull;
@@ -818,50 +766,34 @@ constexpr int MAX_SPLIT_LG = PT_MAX_SPLIT_LG;
 __device__ __forceinline__ int itemTile(int item) { return item & ((1 << ITEM_TILE_BITS) - 1); }
 __device__ __forceinline__ int itemSub(int item) { return (item >> ITEM_TILE_BITS) & 63; }
 __device__ __forceinline__ int itemLg(int item) { return (item >> 28) & 7; }
+// A batch of nFrames frames (RenderParams::nFrames): claim `it` of queue q is work item
+// it / nFrames of the band for frame it % nFrames, so a band's claims cover its items once
+// per frame and the frames of one item are claimed one after another (set in *frame).
 struct TileCursor {
   int qi = 0;  // queues found empty (wave-uniform)
-  __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home, const int* order = nullptr,
-                                      int orderCap = 0) {
+  __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home, int& frame, int nFrames = 1,
+                                      const int* order = nullptr, int orderCap = 0) {
     while (qi < NUM_QUEUES) {
       const int q = (home + qi) & (NUM_QUEUES - 1);
       int it = 0;
       if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
       it = __shfl(it, 0, 64);
+      const int k = nFrames == 1 ? it : it / nFrames;
       if (order) {
-        if (it < order[NUM_QUEUES * orderCap + q]) return order[q * orderCap + it];
+        if (it < order[NUM_QUEUES * orderCap + q] * nFrames) {
+          frame = it - k * nFrames;
+          return order[q * orderCap + k];
+        }
       } else {
-        const int t = q * perQueue + it;
-        if (it < perQueue && t < numItems) return t;
+        const int t = q * perQueue + k;
+        if (k < perQueue && t < numItems) {
+          frame = it - k * nFrames;
+          return t;
+        }
       }
       qi++;
     }
     return -1;
-  }
-  // Claim ahead (PT_CLAIM_AHEAD): the home queue's next slot is claimed when a
-  // tile starts and resolved when it ends, so the device-scope atomic's round
-  // trip overlaps the tile's own fetches instead of preceding them.
-  int ahead = -1;  // lane 0: the claimed slot of queue (home + qi), -1 = none outstanding
-  __device__ __forceinline__ void claimAhead(int* queue, int home) {
-    if (qi < NUM_QUEUES && (threadIdx.x & 63) == 0)
-      ahead = atomicAdd(queue + ((home + qi) & (NUM_QUEUES - 1)) * CTL_LINE_INTS, 1);
-  }
-  __device__ __forceinline__ int nextAhead(int* queue, int perQueue, int numItems, int home, const int* order,
-                                           int orderCap) {
-    if (qi < NUM_QUEUES) {
-      const int it = __shfl(ahead, 0, 64);
-      ahead = -1;
-      if (it >= 0) {
-        const int q = (home + qi) & (NUM_QUEUES - 1);
-        if (order) {
-          if (it < order[NUM_QUEUES * orderCap + q]) return order[q * orderCap + it];
-        } else {
-          const int t = q * perQueue + it;
-          if (it < perQueue && t < numItems) return t;
-        }
-        qi++;
-      }
-    }
-    return next(queue, perQueue, numItems, home, order, orderCap);
   }
 };
 

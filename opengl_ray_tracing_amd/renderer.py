@@ -63,6 +63,8 @@ class FrameStats:
     accel_nodes: int = 0
     accel_depth: int = 0
     regen: int = 0
+    frames: int = 0       # frames rendered (a batch launch renders several)
+    frame_batch: int = 1  # most frames per launch
 
 
 def _fp(a: np.ndarray):
@@ -79,10 +81,11 @@ class Renderer:
     def __init__(self, width: int, height: int, integrator="lambert", max_bounce: int = -1, device: int = 0,
                  tile_rank: int = 0, tile_world: int = 1, tile_size: int = 32, flags: int = 0,
                  basic_samples: int = 128, basic_seed: int = 0, sample_rank: int = 0, sample_world: int = 1,
-                 devices=None, gather="auto"):
+                 devices=None, gather="auto", frame_batch: int = 0):
         """devices: a list of HIP device ids (2..8, repeats allowed) makes this one context render
         screen tiles on all of them and gather them into the first device's accumulation every
-        frame (pt_config.n_devices; gather "auto" / "copy" / "rccl")."""
+        frame (pt_config.n_devices; gather "auto" / "copy" / "rccl"). frame_batch: most frames per
+        launch of render_frames (0 = automatic: tile_world frames of a screen-tile share)."""
         self._lib = _native.load()
         cfg = _native.PtConfig()
         cfg.width, cfg.height = int(width), int(height)
@@ -102,6 +105,9 @@ class Renderer:
                 cfg.device_ids[k] = int(d)
             cfg.device_id = int(devices[0])
         cfg.gather = GATHER[gather] if isinstance(gather, str) else int(gather)
+        cfg.frame_batch = int(frame_batch)
+        from . import HW_QUEUES  # the queues GPU_MAX_HW_QUEUES granted this process (package import)
+        cfg.hw_queues = int(HW_QUEUES)
         h = C.c_void_p()
         _native.check(self._lib.pt_create(C.byref(h), C.byref(cfg)), None, "pt_create")
         self._h = h
@@ -174,6 +180,12 @@ class Renderer:
                                                off.ctypes.data_as(C.POINTER(C.c_int64)), off.size),
                  "pt_set_basic_stream")
 
+    def set_basic_image(self, img: np.ndarray):
+        """BASIC checkpoint restore: the double image (h, w, 3) as basic_image() returned it."""
+        a = np.ascontiguousarray(img, np.float64).reshape(self.height, self.width, 3)
+        self._ck(self._lib.pt_upload_basic_image(self._h, a.ctypes.data_as(_native.c_double_p)),
+                 "pt_upload_basic_image")
+
     def basic_replay_overruns(self) -> int:
         c = C.c_int64()
         self._ck(self._lib.pt_basic_replay_overruns(self._h, C.byref(c)), "pt_basic_replay_overruns")
@@ -190,6 +202,14 @@ class Renderer:
         self._ck(self._lib.pt_render_frame(self._h, _fp(e), _fp(r), int(frame_counter) & 0xFFFFFFFF,
                                            None if out is None else _fp(out)), "pt_render_frame")
         return out
+
+    def render_frames(self, eye, camera_rotate, frame_counter: int, n: int):
+        """n display() calls of one camera (frames frame_counter .. frame_counter + n - 1), rendered
+        in batches (pt_render_frames_async; bit for bit n render_frame calls). Asynchronous."""
+        e = np.ascontiguousarray(eye, np.float32)
+        r = np.ascontiguousarray(camera_rotate, np.float32).reshape(16)
+        self._ck(self._lib.pt_render_frames_async(self._h, _fp(e), _fp(r), int(frame_counter) & 0xFFFFFFFF, int(n)),
+                 "pt_render_frames_async")
 
     def trace_closest(self, rays: np.ndarray):
         r = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
@@ -279,7 +299,8 @@ class Renderer:
         return FrameStats(s.rays, s.node_fetch, s.tri_fetch, s.mat_fetch, s.tex_fetch, s.kernel_ms,
                           s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
                           s.waves_per_simd, s.devices, s.gather, s.frames_in_flight, s.upload_ms,
-                          s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth, s.regen)
+                          s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth, s.regen, s.frames,
+                          s.frame_batch)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")

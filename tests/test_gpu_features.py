@@ -104,6 +104,43 @@ def test_basic_replay_equals_reference_image():
     assert int(st.rays) == c.rays == 914124
 
 
+def test_basic_checkpoint_restore_continues_the_image():
+    """BASIC checkpoints: frames 0..4, the double image downloaded (pt_download_basic_image) and
+    restored into a fresh context (pt_upload_basic_image), frames 5..9 there -- the double image
+    and the f32 sums equal ten uninterrupted frames bit for bit. A restore from the f32 sums
+    (pt_upload_accum, the generic checkpoint) sets the double image the next frame adds to: the
+    sums widened."""
+    sh = scenes.cornell_shapes()
+    w, h = 96, 80
+    z, eye4 = np.zeros(3, np.float32), np.eye(4, dtype=np.float32)
+
+    def ctx():
+        r = Renderer(w, h, "basic", basic_samples=10)
+        r.upload_shapes(sh)
+        return r
+
+    with ctx() as r:
+        for k in range(10):
+            r.render_frame(z, eye4, k, sync=False)
+        full_img, full_acc = r.basic_image(), r.accum()
+    with ctx() as r:
+        for k in range(5):
+            r.render_frame(z, eye4, k, sync=False)
+        img5, acc5 = r.basic_image(), r.accum()
+    with ctx() as r:
+        r.set_basic_image(img5)
+        assert np.array_equal(r.accum()[..., :3], img5.astype(np.float32))
+        for k in range(5, 10):
+            r.render_frame(z, eye4, k, sync=False)
+        assert np.array_equal(r.basic_image().view(np.uint64), full_img.view(np.uint64))
+        assert np.array_equal(r.accum().view(np.uint32), full_acc.view(np.uint32))
+    with ctx() as r:
+        r.set_accum(acc5)
+        assert np.array_equal(r.basic_image(), acc5[..., :3].astype(np.float64))
+        r.render_frame(z, eye4, 5)
+        assert not np.array_equal(r.accum(), acc5)  # the frame added to the restored sums
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_tile_shards_reassemble_bit_exact(world):
     cfg, tris, nodes, hdr = scenes.build_config("c2")

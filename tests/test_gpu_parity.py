@@ -298,45 +298,50 @@ def test_pipelined_frames_equal_serial_frames(request, monkeypatch, name, tile, 
     assert sa.rays == sb.rays
 
 
-@pytest.mark.parametrize("name,tile,flags", [("c4", (0, 8), 0), ("c2", (3, 8), 0), ("c2", (0, 1), 0),
-                                              ("c4", (1, 4), "primary"), ("c2", (0, 8), "mixkernel")])
-def test_kernel_running_mean_equals_serial_frames(request, monkeypatch, name, tile, flags):
-    """The running mean updated inside the frame kernels (pt_kernels.hip completeItem: a tile's
-    last item of a frame mixes the tile in frame order, handing on to later frames that
-    completed it first) gives the images and ray counts of serial frames bit for bit: on small
-    screen-tile shares (where frames in flight overlap most), a whole frame, with the
-    camera-ray pass, and against mixKernel per frame (PT_KERNEL_MIX=0) -- with images read
-    mid-stream and after a clear of the accumulation."""
-    from opengl_ray_tracing_amd import FLAG_PRIMARY_PASS, FLAG_SERIAL_FRAMES
-    monkeypatch.setenv("PT_PIPE_DEPTH", "8")
-    monkeypatch.setenv("PT_KERNEL_MIX", "1")  # opt-in (measured slower than mixKernel, DESIGN.md 4)
-    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL
+@pytest.mark.parametrize("name,tile,batch,flags", [("c4", (0, 8), 0, 0), ("c2", (3, 8), 0, 0), ("c2", (0, 1), 3, 0),
+                                                   ("c4", (1, 4), 4, "primary"), ("c2m", (0, 8), 8, 0),
+                                                   ("c3", (2, 8), 5, "regen")])
+def test_frame_batches_equal_serial_frames(request, name, tile, batch, flags):
+    """Batches of frames (pt_render_frames_async: several frames of one camera per launch, their
+    running-mean updates applied together pixel by pixel in frame order) give the images and ray
+    counts of serial frames bit for bit: small screen-tile shares (the automatic batch, tile_world
+    frames), a whole frame, the camera-ray pass, the megakernel and the regen kernel, batches that
+    straddle the policy probe and a camera restart, images read between batches and after a clear."""
+    from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_PRIMARY_PASS, FLAG_REGEN, FLAG_SERIAL_FRAMES
+    extra = {"primary": FLAG_PRIMARY_PASS | FLAG_MEGAKERNEL, "regen": FLAG_REGEN}.get(flags, 0)
+    if name == "c2m":
+        name, extra = "c2", FLAG_MEGAKERNEL
     cfg, tris, nodes, hdr = request.getfixturevalue(name)
     eye, rot = orbit_camera(*cfg.camera)
+    eye2, rot2 = orbit_camera(30.0, 15.0, 4.0)
     w, h = 960, 540
-    extra = (FLAG_PRIMARY_PASS if flags == "primary" else 0) | FLAG_MEGAKERNEL  # the protocol is the megakernel's
+    # (camera, first frame, frames): the probe's frames, then batches of varied sizes, a restart
+    calls = [((eye, rot), 0, 7), ((eye, rot), 7, 16), ((eye, rot), 23, 9), ((eye, rot), 32, 24),
+             ((eye2, rot2), 0, 1), ((eye2, rot2), 1, 30), ((eye2, rot2), 31, 11)]
 
-    def run(fl):
+    def run(fl, batched):
         out = []
         with Renderer(w, h, cfg.integrator, max_bounce=cfg.max_bounce, flags=fl | extra, tile_rank=tile[0],
-                      tile_world=tile[1]) as r:
+                      tile_world=tile[1], frame_batch=batch) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
-            for f in range(64):
-                r.render_frame(eye, rot, f, sync=False)
-                if f == 40:
+            for k, ((e, m), f0, n) in enumerate(calls):
+                if batched:
+                    r.render_frames(e, m, f0, n)
+                else:
+                    for f in range(f0, f0 + n):
+                        r.render_frame(e, m, f, sync=False)
+                if k in (2, 3, 5):
                     out.append(r.accum())
-                if f == 50:
+                if k == 3:
                     r.clear()
             out.append(r.accum())
             return out, r.stats()
 
-    a, sa = run(0)
-    if flags == "mixkernel":
-        monkeypatch.setenv("PT_KERNEL_MIX", "0")
-        b, sb = run(0)
-    else:
-        b, sb = run(FLAG_SERIAL_FRAMES)
+    a, sa = run(0, True)
+    b, sb = run(FLAG_SERIAL_FRAMES, False)
+    assert sa.frames == sb.frames == sum(c[2] for c in calls)
+    assert sa.frame_batch == (batch or tile[1]) and sa.launches < sa.frames
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert sa.rays == sb.rays

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Per-rank frame time of the screen-tile split, measured on one GPU: rank 0's
 share of an N-way split (its 32x32 tiles t % N == 0) rendered alone, wall ms per
-frame with frames in flight. The N-GPU frame is at least this plus whatever of
-the per-frame gather does not overlap the next frame.
+frame with frames in flight and frames batched per launch (pt_render_frames_async,
+PT_BATCH frames per launch, 0 = the renderer's choice: N). The N-GPU frame is at
+least this plus whatever of the per-batch gather does not overlap the next batch.
 
-    [PT_VARIANT=<tuning build>] python tools/shard_time.py [config] [N ...]
+    [PT_VARIANT=<tuning build>] [PT_BATCH=b] python tools/shard_time.py [config] [N ...]
 """
 import json
 import sys
@@ -30,28 +31,28 @@ def main():
     from opengl_ray_tracing_amd import Renderer, orbit_camera, scenes
     cfg, tris, nodes, hdr = scenes.build_config(cfg_name)
     eye, rot = orbit_camera(*cfg.camera)
+    batch = int(os.environ.get("PT_BATCH", "0"))
     for n in worlds:
         with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, tile_rank=0,
-                      tile_world=n) as r:
+                      tile_world=n, frame_batch=batch) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
-            for f in range(100):  # policy probe (tree, split, order, depth) + warmup
-                r.render_frame(eye, rot, f, sync=False)
+            r.render_frames(eye, rot, 0, 100)  # policy probe (tree, split, order) + warmup
             r.synchronize()
             r.reset_stats()
-            K = 100
+            K = 200
             t0 = time.perf_counter()
-            for f in range(100, 100 + K):
-                r.render_frame(eye, rot, f, sync=False)
+            r.render_frames(eye, rot, 100, K)
             t_sub = time.perf_counter()
             r.synchronize()
             ms = 1e3 * (time.perf_counter() - t0) / K
             submit_ms = 1e3 * (t_sub - t0) / K  # host time per pt_render_frame_async call
             st = r.stats()
         print(json.dumps({"variant": os.environ.get("PT_VARIANT", "base"), "config": cfg_name, "world": n, "rank0_ms_per_frame": round(ms, 4),
+                          "frames": st.frames, "launches": st.launches, "frame_batch": st.frame_batch,
                           "kernel_ms_avg": round(st.kernel_ms_total / max(st.launches, 1), 4),
                           "host_submit_ms": round(submit_ms, 4),
-                          "rays_per_frame": st.rays // max(st.launches, 1),
+                          "rays_per_frame": st.rays // max(st.frames, 1),
                           "frames_in_flight": st.frames_in_flight}), flush=True)
 
 
