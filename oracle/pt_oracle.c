@@ -759,61 +759,80 @@ static void bfill(BHit* r, const double* sh) {
   r->specularRate = sh[17]; r->roughness = sh[18]; r->refractRate = sh[19];
   r->refractAngle = sh[20]; r->refractRoughness = sh[21];
 }
-/* Triangle::intersect B:90-122 */
-static BHit b_tri(const double* sh, v3 S, v3 d) {
-  BHit res; memset(&res, 0, sizeof(res));
+/* Triangle::intersect B:90-122: the accept test and distance; the winner's normal
+ * (n, flipped to face the ray) and material are filled in once by b_shoot. */
+static int b_tri(const double* sh, v3 S, v3 d, float* tOut, v3* POut) {
   v3 p1 = V3((float)sh[1], (float)sh[2], (float)sh[3]), p2 = V3((float)sh[4], (float)sh[5], (float)sh[6]);
   v3 p3 = V3((float)sh[7], (float)sh[8], (float)sh[9]);
   v3 n = V3((float)sh[13], (float)sh[14], (float)sh[15]);
   v3 N = n;
   if (dot(N, d) > 0.0f) N = neg(N);
-  if (fabsf(dot(N, d)) < 0.00001f) return res;
+  if (fabsf(dot(N, d)) < 0.00001f) return 0;
   float t = (dot(N, p1) - dot(S, N)) / dot(d, N);
-  if (t < 0.0005f) return res;
+  if (t < 0.0005f) return 0;
   v3 P = add(S, scl(d, t));
   v3 c1 = cross(sub(p2, p1), sub(P, p1));
   v3 c2 = cross(sub(p3, p2), sub(P, p2));
   v3 c3 = cross(sub(p1, p3), sub(P, p3));
-  if (dot(c1, n) < 0 || dot(c2, n) < 0 || dot(c3, n) < 0) return res;
-  res.isHit = 1; res.distance = t; res.hitPoint = P;
-  bfill(&res, sh);
-  res.normal = N;
-  return res;
+  if (dot(c1, n) < 0 || dot(c2, n) < 0 || dot(c3, n) < 0) return 0;
+  *tOut = t;
+  *POut = P;
+  return 1;
 }
 /* Sphere::intersect B:135-164: OS, SH, t are float (glm length / dot); pow(x, 2)
  * of a float is exact in double; R is double, so OH > R and PH are double
  * expressions (pow(R, 2) == R * R for the scene's radii, test_basic_sphere_pow);
  * length(SH) of a float is |SH|. */
-static BHit b_sphere(const double* sh, v3 S, v3 d) {
-  BHit res; memset(&res, 0, sizeof(res));
+static int b_sphere(const double* sh, v3 S, v3 d, float* tOut, v3* POut) {
   v3 O = V3((float)sh[1], (float)sh[2], (float)sh[3]);
   double R = sh[22];
   v3 OSv = sub(O, S);
   float OS = sqrtf(dot(OSv, OSv));
   float SH = dot(OSv, d);
   float OH = (float)sqrt((double)OS * (double)OS - (double)SH * (double)SH);
-  if ((double)OH > R) return res;
+  if ((double)OH > R) return 0;
   float PH = (float)sqrt(R * R - (double)OH * (double)OH);
   float t1 = fabsf(SH) - PH;
   float t2 = fabsf(SH) + PH;
   float t = (t1 < 0) ? t2 : t1;
   v3 P = add(S, scl(d, t));
-  if (fabsf(t1) < 0.0005f || fabsf(t2) < 0.0005f) return res;
-  res.isHit = 1; res.distance = t; res.hitPoint = P;
-  bfill(&res, sh);
-  res.normal = normalize(sub(P, O));
-  return res;
+  if (fabsf(t1) < 0.0005f || fabsf(t2) < 0.0005f) return 0;
+  *tOut = t;
+  *POut = P;
+  return 1;
 }
-/* shoot B:192-205 (res.distance is a double initialised from 1145141919.810f) */
+/* shoot B:192-205 (res.distance is a double initialised from 1145141919.810f): the
+ * first shape at the least distance wins; only its HitResult is formed */
 static BHit b_shoot(Ctx* cx, v3 S, v3 d) {
   const orc_scene* s = cx->s;
-  BHit res; memset(&res, 0, sizeof(res));
+  BHit res;
+  res.isHit = 0;
   res.distance = (double)1145141919.810f;
   cx->c.rays++;
+  int win = -1;
+  v3 wP = V3(0, 0, 0);
   for (int k = 0; k < s->nShapes; k++) {
     const double* sh = s->shapes + (size_t)k * ORC_SHAPE_DOUBLES;
-    BHit r = (sh[0] == 1.0) ? b_sphere(sh, S, d) : b_tri(sh, S, d);
-    if (r.isHit && r.distance < res.distance) res = r;
+    float t;
+    v3 P;
+    const int h = (sh[0] == 1.0) ? b_sphere(sh, S, d, &t, &P) : b_tri(sh, S, d, &t, &P);
+    if (h && (double)t < res.distance) {
+      res.distance = t;
+      win = k;
+      wP = P;
+    }
+  }
+  if (win < 0) return res;
+  const double* sh = s->shapes + (size_t)win * ORC_SHAPE_DOUBLES;
+  res.isHit = 1;
+  res.hitPoint = wP;
+  bfill(&res, sh);
+  if (sh[0] == 1.0) {
+    res.normal = normalize(sub(wP, V3((float)sh[1], (float)sh[2], (float)sh[3])));
+  } else {
+    v3 N = V3((float)sh[13], (float)sh[14], (float)sh[15]);
+    if (dot(N, d) > 0.0f) N = neg(N);
+    res.normal = N;
   }
   return res;
 }

@@ -1,0 +1,31 @@
+"""The CPU baseline's fairness gate (BASELINE.md "Fairness gate"): the CPU restatement's BASIC mode
+(oracle/pt_oracle.c, BasicRayTracingWithC++/main.cpp:192-205 shoot, :359-432 the pixel loop) must
+reach >= 1.5 Mrays/s per core on C1 (256 x 256, 4 spp, the Cornell box), so that the GPU is
+compared against a CPU tracer as fast as the reference's own (1.59 Mrays/s in the survey
+container). Timed single-threaded with the per-pixel counter RNG (the parallel baseline's mode),
+best of three runs, as bench.py's cpu_baseline runs the same library."""
+import time
+
+import numpy as np
+
+import oracle
+from opengl_ray_tracing_amd import scenes
+
+GATE_MRAYS_PER_CORE = 1.5
+
+
+def test_basic_mode_meets_the_fairness_gate():
+    o = oracle.Oracle(shapes=scenes.cornell_shapes())
+    w = h = 256
+    best = 0.0
+    for _ in range(3):
+        acc = np.zeros((h, w, 4), np.float32)
+        rays = 0
+        t0 = time.perf_counter()
+        for k in range(4):
+            acc, c = o.render(w, h, "basic", k, accum=acc, basic_samples=4, threads=1)
+            rays += c.rays
+        best = max(best, rays / (time.perf_counter() - t0) / 1e6)
+    print(f"BASIC counter mode, 1 thread: {best:.2f} Mrays/s (gate {GATE_MRAYS_PER_CORE})")
+    assert rays > 900_000  # ~914k rays: 256 x 256 x 4 camera rays plus the paths' bounces
+    assert best >= GATE_MRAYS_PER_CORE
