@@ -264,13 +264,13 @@ def main():
         # running-mean update) instead
         pipelined = st.frames_in_flight > 1
         roofline = make_roofline(args, cfg, ms_per_step if pipelined else kernel_ms_avg, rays_per_frame,
-                                 bytes_per_ray, n)
+                                 bytes_per_ray, n, "frame")
         roofline["time_basis"] = ("wall ms per frame (frames in flight)" if pipelined
                                   else "frame kernel HIP-event ms")
         roofline["launch_ms"] = round(kernel_ms_avg, 4)
         roofline["kernel"] = ("regenKernel<%s>" if st.regen else "renderKernel<%s>") % cfg.integrator
         if serial_ms is not None:
-            kb = make_roofline(args, cfg, serial_ms, rays_per_frame, bytes_per_ray, n)
+            kb = make_roofline(args, cfg, serial_ms, rays_per_frame, bytes_per_ray, n, "frame_serial")
             roofline["kernel_basis"] = {
                 "time_basis": "frame kernel HIP-event ms, frames issued serially (PT_FLAG_SERIAL_FRAMES)",
                 "kernel_ms": round(serial_ms, 4), "frames": SERIAL_FRAMES, "bound": kb["bound"],
@@ -314,11 +314,14 @@ def main():
         dist.destroy_process_group()
 
 
-def make_roofline(args, cfg, kernel_ms, rays_per_frame, bytes_per_ray, n):
-    """Roofline of the frame kernel. Each resource's per-launch work comes from the hardware
-    counters of the same workload (profiles/r3/counters.json, tools/roofline.py, one rocprofv3
-    pass per counter group over this bench's timed frames); divided by this run's live kernel
-    time it gives the achieved rate:
+def make_roofline(args, cfg, kernel_ms, rays_per_frame, bytes_per_ray, n, basis="frame"):
+    """Roofline of a frame. Each resource's work per frame comes from the hardware counters of the
+    same workload (profiles/<round>/counters.json, tools/roofline.py, one rocprofv3 pass per counter
+    group over this bench's timed frames), summed over every kernel of the frame (basis "frame":
+    camera-ray pass, frame kernel, tile reorder, running-mean update -- over the wall time per
+    frame) or over the kernels of a serially issued frame ("frame_serial": no running-mean update
+    kernel -- over their summed HIP-event time); divided by this run's live time it gives the
+    achieved rate:
       valu: SQ_INSTS_VALU wave-instructions / t  vs 1228.8 G/s (1024 SIMDs x 2.4 GHz / 2 cycles)
       hbm:  (2*FETCH_SIZE + WRITE_SIZE) KiB / t  vs 8 TB/s (gfx950 FETCH_SIZE halving corrected)
     `bound` is the resource with the higher fraction. `equivalent_GBs` is the reference
@@ -337,18 +340,20 @@ def make_roofline(args, cfg, kernel_ms, rays_per_frame, bytes_per_ray, n):
     if not ent:
         return {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
                 "note": "no committed counters for this workload", **base}
+    work = ent.get(basis) or {"kernels": ["frame"], "valu_insts": ent["valu_insts"], "dram_bytes": ent["dram_bytes"]}
     cands = {
-        "valu": (ent["valu_insts"] / t / 1e9, VALU_PEAK_GINST, "G VALU wave-instructions/s"),
-        "hbm": (ent["dram_bytes"] / t / 1e9, HBM_PEAK_GBS, "GB/s"),
+        "valu": (work["valu_insts"] / t / 1e9, VALU_PEAK_GINST, "G VALU wave-instructions/s"),
+        "hbm": (work["dram_bytes"] / t / 1e9, HBM_PEAK_GBS, "GB/s"),
     }
     bound = max(cands, key=lambda k: cands[k][0] / cands[k][1])
     a, pk, unit = cands[bound]
     return {"bound": bound, "achieved": round(a, 2), "peak": pk, "unit": unit, "frac": round(a / pk, 4),
-            "traffic": int(ent["dram_bytes"]),
+            "traffic": int(work["dram_bytes"]),
             "candidates": {k: {"achieved": round(v[0], 2), "peak": v[1], "unit": v[2], "frac": round(v[0] / v[1], 4)}
                            for k, v in cands.items()},
             "counters": {"source": str(p.relative_to(ROOT)) if p.is_relative_to(ROOT) else str(p),
-                         "valu_insts_per_launch": ent["valu_insts"], "dram_bytes_per_launch": ent["dram_bytes"],
+                         "kernels": work["kernels"], "valu_insts_per_frame": work["valu_insts"],
+                         "dram_bytes_per_frame": work["dram_bytes"],
                          "l2_hit": ent.get("l2_hit"), "profiled_kernel_ms": ent.get("kernel_ms")},
             **base}
 

@@ -19,9 +19,10 @@ echo "trace=$rc"; [ $rc -eq 0 ] || exit $rc
 SERIAL=(python3 "$REPO/bench.py" --config "$CFG" --steps 30 --warmup 5 --no-cpu-baseline --no-psnr --no-reset --no-serial --flags 128)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/serial" -o run -- "${SERIAL[@]}" > "$OUT/serial_line.json" 2> "$OUT/serial.log"; rc=$?
 echo "serial=$rc"; [ $rc -eq 0 ] || exit $rc
-# counters over serially issued frames (full-residency grid, one frame at a time: the interval the
-# counters cover is the kernel's own duration, comparable with the serial trace above)
-BENCHC=(python3 "$REPO/bench.py" --config "$CFG" --steps 10 --warmup 2 --no-cpu-baseline --no-psnr --no-reset --no-serial --flags 128)
+# counters over the bench's own (pipelined) frames: a --pmc pass serialises the dispatches, so each
+# frame kernel's counters -- camera-ray pass, frame kernel, tile reorder, running-mean update --
+# cover its own dispatch (tools/roofline.py sums them per frame)
+BENCHC=(python3 "$REPO/bench.py" --config "$CFG" --steps 10 --warmup 2 --no-cpu-baseline --no-psnr --no-reset --no-serial)
 PASSES=(
   "fetch:FETCH_SIZE"
   "write:WRITE_SIZE"

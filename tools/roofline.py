@@ -1,28 +1,32 @@
 #!/usr/bin/env python3
-"""Roofline evidence from the rocprofv3 runs of tools/gpu_profile.sh.
+"""Roofline evidence from the rocprofv3 runs of tools/gpu_profile.sh, over every kernel of a frame.
 
     python tools/roofline.py <tag> <cfg> [<cfg> ...]
 
 Reads gpurun_out/prof_<tag>_<cfg>/ and writes, under profiles/<tag>/:
-  <cfg>/kernel_stats.csv       rocprofv3 --kernel-trace --stats summary of the bench command
-  <cfg>/timed_dispatches.json  the bench kernel's dispatches of bench.py's timed region
-  <cfg>/counters.csv           every counter row of the bench kernel's timed dispatches
-  bench_<cfg>.json             the profiled run's bench line
-  counters.json                {cfg: per-launch counter averages + the derived roofline work}
-bench.py reads counters.json (--counters) and divides each resource's per-launch
-work by its own live kernel time.
+  <cfg>/kernel_stats.csv        rocprofv3 --kernel-trace --stats summary of the bench command
+  <cfg>/kernel_stats_serial.csv the same with frames issued serially (PT_FLAG_SERIAL_FRAMES)
+  <cfg>/timed_dispatches.json   each frame kernel's dispatches of bench.py's timed frames
+  <cfg>/counters.csv            every counter row of those dispatches
+  bench_<cfg>.json              the profiled run's bench line
+  counters.json                 {cfg: per-kernel and per-frame counter work, time bases}
 
-The bench kernel is the culling frame kernel renderKernel<I, true, false[, W]>
-(or, for large Disney/MIS scenes, the path-regeneration kernel regenKernel<I, true[, W]>).
-bench.py renders PROBE_FRAMES policy-probe frames, then W warmup and K timed
-frames of it, so its timed dispatches are numbers [PROBE+W, PROBE+W+K) in
-dispatch order (the fetch-counting kernel, renderKernel<I, false, true>, and
-the PSNR check's basicKernel are other kernels).
+A frame (bench.py step at N = 1) runs these kernels, each once (FRAME_KERNELS): the camera-ray
+pass primaryKernel (the regen path), the frame kernel (renderKernel<I, true, false[, W]> or
+regenKernel<I, true[, W, true]>), the tile reorder reorderKernel (megakernel frames in
+longest-first order) and the running-mean update mixKernel. The profiled bench runs end with its
+timed frames (--no-reset --no-serial --no-psnr), so each kernel's last K dispatches are the timed
+frames' (K = the run's --steps).
 
-Derived per-launch work (MI355X_MICROARCH.md):
+Per kernel (averaged over its timed dispatches of each pass) and summed per frame:
   valu_insts = SQ_INSTS_VALU (wave64 instructions; peak issue 1024 SIMDs x 2.4 GHz / 2 cycles)
   dram_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   (KiB units; gfx950 FETCH_SIZE halving)
-  l2_hit     = TCC_HIT / (TCC_HIT + TCC_MISS);  clock_ghz = GRBM_GUI_ACTIVE / 8 / dispatch time, per sq-pass dispatch
+  l2_hit     = TCC_HIT / (TCC_HIT + TCC_MISS)
+Time bases: the pipelined trace's wall time per frame is bench.py's (ms_per_step); the summed
+serial-trace durations of the frame's kernels (frames issued one after another, accumulating in
+place: no mixKernel) are its kernel basis -- divided into the work of the same kernels.
+bench.py reads counters.json (--counters): frame.valu_insts / frame.dram_bytes over the wall time,
+frame_serial.* over the serial kernel time.
 """
 import csv
 import glob
@@ -35,10 +39,14 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "gpurun_out"
-PROBE = 90  # bench.py PROBE_FRAMES: policy-probe frames ahead of the warmup and timed frames
-TRACE_RUN = (5, 30)    # tools/gpu_profile.sh: --warmup 5 --steps 30 under --kernel-trace
-COUNTER_RUN = (2, 10)  # --warmup 2 --steps 10 under each --pmc pass
-BENCH_KERNEL = re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true(, \d+)?(, (true|false))?>")
+TRACE_STEPS = 30    # tools/gpu_profile.sh: --steps 30 under --kernel-trace (pipelined and serial)
+COUNTER_STEPS = 10  # --steps 10 under each --pmc pass
+FRAME_KERNELS = {
+    "primary": re.compile(r"primaryKernel"),
+    "frame": re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true(, \d+)?(, (true|false))?>"),
+    "reorder": re.compile(r"reorderKernel"),
+    "mix": re.compile(r"mixKernel"),
+}
 
 
 def one(pattern: str) -> Path:
@@ -48,10 +56,25 @@ def one(pattern: str) -> Path:
     return Path(hits[0])
 
 
-def timed(rows, run):
-    w, k = run
-    rows = sorted(rows, key=lambda r: int(r["Dispatch_Id"]))
-    return rows[PROBE + w:PROBE + w + k], len(rows)
+def kind_of(name):
+    for k, rx in FRAME_KERNELS.items():
+        if rx.search(name):
+            return k
+    return None
+
+
+def last_dispatches(rows, k):
+    """{kind: the last k dispatches of that frame kernel, in dispatch order}"""
+    by = defaultdict(list)
+    for r in rows:
+        kd = kind_of(r["Kernel_Name"])
+        if kd:
+            by[kd].append(r)
+    return {kd: sorted(v, key=lambda r: int(r["Dispatch_Id"]))[-k:] for kd, v in by.items()}
+
+
+def dur_ms(r):
+    return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
 
 
 def main():
@@ -65,86 +88,101 @@ def main():
         d = dst / c
         d.mkdir(exist_ok=True)
         shutil.copy(one(f"{prof}/trace/**/run_kernel_stats.csv"), d / "kernel_stats.csv")
-        trace = [r for r in csv.DictReader(open(one(f"{prof}/trace/**/run_kernel_trace.csv")))
-                 if BENCH_KERNEL.search(r["Kernel_Name"])]
-        sel, total = timed(trace, TRACE_RUN)
-        ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in sel]
-        kernel_ms = sum(ms) / len(ms)
+        trace = list(csv.DictReader(open(one(f"{prof}/trace/**/run_kernel_trace.csv"))))
+        sel = last_dispatches(trace, TRACE_STEPS)
+        serial = {}
+        sp = sorted(glob.glob(f"{prof}/serial/**/run_kernel_trace.csv", recursive=True))
+        if sp:
+            serial = last_dispatches(list(csv.DictReader(open(sp[0]))), TRACE_STEPS)
+            shutil.copy(one(f"{prof}/serial/**/run_kernel_stats.csv"), d / "kernel_stats_serial.csv")
+        disp = {}
+        for kd, rows in sel.items():
+            ms = [dur_ms(r) for r in rows]
+            disp[kd] = {"kernel": rows[-1]["Kernel_Name"], "timed_dispatches": len(rows),
+                        "avg_ms_pipelined": round(sum(ms) / len(ms), 4), "min_ms_pipelined": round(min(ms), 4),
+                        "vgpr": rows[-1].get("VGPR_Count"), "scratch": rows[-1].get("Scratch_Size")}
+            if kd in serial:
+                sms = [dur_ms(r) for r in serial[kd]]
+                disp[kd]["avg_ms_serial"] = round(sum(sms) / len(sms), 4)
         (d / "timed_dispatches.json").write_text(json.dumps({
-            "kernel": sel[-1]["Kernel_Name"], "dispatches": total, "timed_dispatches": len(sel),
-            "selection": f"dispatches [{PROBE}+{TRACE_RUN[0]}, +{TRACE_RUN[1]}) of the bench kernel",
-            "timed_avg_ms": round(kernel_ms, 4), "timed_ms": [round(x, 4) for x in ms],
-            "vgpr": sel[-1].get("VGPR_Count"), "scratch": sel[-1].get("Scratch_Size")}, indent=1) + "\n")
+            "selection": f"the last {TRACE_STEPS} dispatches of each frame kernel (the bench's timed frames)",
+            "kernels": disp}, indent=1) + "\n")
         line = (prof / "bench_line.json").read_text().strip().splitlines()
         line = [ln for ln in line if ln.startswith("{")]
         if line:
             (dst / f"bench_{c}.json").write_text(line[-1] + "\n")
 
-        vals = defaultdict(list)
+        vals = {kd: defaultdict(list) for kd in FRAME_KERNELS}
         rows_out = []
         header = None
         for name in ("fetch", "write", "sq", "mem"):
-            f = one(f"{prof}/{name}/**/run_counter_collection.csv")
-            rows = list(csv.DictReader(open(f)))
+            rows = list(csv.DictReader(open(one(f"{prof}/{name}/**/run_counter_collection.csv"))))
             header = header or list(rows[0].keys())
-            bench = [r for r in rows if BENCH_KERNEL.search(r["Kernel_Name"])]
             by_disp = defaultdict(list)
-            for r in bench:
-                by_disp[r["Dispatch_Id"]].append(r)
-            disp = sorted(by_disp, key=int)
-            w, k = COUNTER_RUN
-            keep = disp[PROBE + w:PROBE + w + k]
-            for di in keep:
-                for r in by_disp[di]:
-                    vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-                    rows_out.append({"pass": name, **r})
-                r0 = by_disp[di][0]
-                if name == "sq" and r0.get("End_Timestamp"):  # the counter pass's own dispatch duration
-                    dms = (int(r0["End_Timestamp"]) - int(r0["Start_Timestamp"])) / 1e6
-                    vals["_counter_dispatch_ms"].append(dms)
-                    # the clock of this dispatch: its own GRBM_GUI_ACTIVE (8 XCDs) over its own duration
-                    # (GRBM_GUI_ACTIVE is also sampled in the mem pass, whose dispatches last differently)
-                    gg = [float(r["Counter_Value"]) for r in by_disp[di] if r["Counter_Name"] == "GRBM_GUI_ACTIVE"]
-                    if gg and dms > 0:
-                        vals["_clock_ghz"].append(gg[0] / 8 / (dms * 1e-3) / 1e9)
+            for r in rows:
+                if kind_of(r["Kernel_Name"]):
+                    by_disp[r["Dispatch_Id"]].append(r)
+            per_kind = defaultdict(list)
+            for di in sorted(by_disp, key=int):
+                per_kind[kind_of(by_disp[di][0]["Kernel_Name"])].append(di)
+            for kd, dis in per_kind.items():
+                for di in dis[-COUNTER_STEPS:]:
+                    for r in by_disp[di]:
+                        vals[kd][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                        rows_out.append({"pass": name, **r})
+                    r0 = by_disp[di][0]
+                    if name == "sq" and r0.get("End_Timestamp"):  # the dispatch's own (serialised) duration
+                        vals[kd]["_dispatch_ms"].append(dur_ms(r0))
         with open(d / "counters.csv", "w", newline="") as fh:
             wr = csv.DictWriter(fh, fieldnames=["pass"] + header)
             wr.writeheader()
             wr.writerows(rows_out)
-        m = {k: sum(v) / len(v) for k, v in vals.items()}
-        g = lambda k: m.get(k, float("nan"))  # noqa: E731
-        cms = m.pop("_counter_dispatch_ms", float("nan"))
-        vals.pop("_counter_dispatch_ms", None)
-        clock = m.pop("_clock_ghz", float("nan"))
-        vals.pop("_clock_ghz", None)
-        # the kernel with nothing overlapping it: the serial-frames trace (PT_FLAG_SERIAL_FRAMES)
-        serial_ms = None
-        sp = sorted(glob.glob(f"{prof}/serial/**/run_kernel_trace.csv", recursive=True))
-        if sp:
-            st = [r for r in csv.DictReader(open(sp[0])) if BENCH_KERNEL.search(r["Kernel_Name"])]
-            ssel, _ = timed(st, TRACE_RUN)
-            sms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in ssel]
-            serial_ms = round(sum(sms) / len(sms), 4)
-            shutil.copy(one(f"{prof}/serial/**/run_kernel_stats.csv"), d / "kernel_stats_serial.csv")
+        kernels = {}
+        for kd, v in vals.items():
+            if not v:
+                continue
+            m = {k: sum(x) / len(x) for k, x in v.items()}
+            g = lambda k: m.get(k, float("nan"))  # noqa: E731
+            kernels[kd] = {
+                "kernel": disp.get(kd, {}).get("kernel"),
+                "valu_insts": round(g("SQ_INSTS_VALU")),
+                "dram_bytes": round((2 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024),
+                "l2_hit": round(g("TCC_HIT_sum") / max(g("TCC_HIT_sum") + g("TCC_MISS_sum"), 1.0), 4),
+                "valu_lane_util": round(g("SQ_THREAD_CYCLES_VALU") / max(64 * g("SQ_ACTIVE_INST_VALU"), 1.0), 4),
+                "counter_dispatch_ms": round(g("_dispatch_ms"), 4),
+                "avg_ms_serial": disp.get(kd, {}).get("avg_ms_serial"),
+                "avg_ms_pipelined": disp.get(kd, {}).get("avg_ms_pipelined"),
+                "counters_per_launch": {k: round(x, 1) for k, x in sorted(m.items()) if not k.startswith("_")},
+            }
+
+        def frame_sum(kinds):
+            ks = [kernels[k] for k in kinds if k in kernels]
+            return {"kernels": [k for k in kinds if k in kernels],
+                    "valu_insts": sum(k["valu_insts"] for k in ks), "dram_bytes": sum(k["dram_bytes"] for k in ks),
+                    "counter_dispatch_ms": round(sum(k["counter_dispatch_ms"] for k in ks), 4)}
+        frame = frame_sum(list(FRAME_KERNELS))
+        fserial = frame_sum([k for k in FRAME_KERNELS if k != "mix"])
+        ser = [kernels[k]["avg_ms_serial"] for k in fserial["kernels"] if kernels[k].get("avg_ms_serial")]
+        fserial["serial_kernel_ms"] = round(sum(ser), 4) if ser else None
+        fk = kernels.get("frame", {})
         ent = {
-            "kernel": sel[-1]["Kernel_Name"], "kernel_ms": round(kernel_ms, 4),
-            "valu_insts": round(g("SQ_INSTS_VALU")),
-            "dram_bytes": round((2 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024),
-            "l2_hit": round(g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")), 4),
-            "valu_lane_util": round(g("SQ_THREAD_CYCLES_VALU") / (64 * g("SQ_ACTIVE_INST_VALU")), 4),
-            # per dispatch of the sq pass: GRBM_GUI_ACTIVE summed over the 8 XCDs over that dispatch's
-            # own (serialised) duration -- the interval its counters describe -- averaged
-            "counter_dispatch_ms": round(cms, 4),
-            "clock_ghz_profiled": round(clock, 3),
-            "serial_kernel_ms": serial_ms,
-            "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())},
-            "samples": {k: len(v) for k, v in sorted(vals.items())},
-            "derivation": "valu_insts = SQ_INSTS_VALU; dram_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024; "
-                          "per launch, averaged over the bench kernel's timed dispatches of each pass",
+            # the frame kernel alone (as rounds 1-3 reported it) ...
+            "kernel": fk.get("kernel"), "valu_insts": fk.get("valu_insts"), "dram_bytes": fk.get("dram_bytes"),
+            "l2_hit": fk.get("l2_hit"), "valu_lane_util": fk.get("valu_lane_util"),
+            "kernel_ms": disp.get("frame", {}).get("avg_ms_pipelined"),
+            "serial_kernel_ms": disp.get("frame", {}).get("avg_ms_serial"),
+            # ... and every kernel of a frame
+            "kernels": kernels,
+            "frame": frame,            # all frame kernels: work over bench.py's wall ms per frame
+            "frame_serial": fserial,   # without mixKernel: work over the serial frames' kernel time
+            "derivation": "per kernel: valu_insts = SQ_INSTS_VALU; dram_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024, "
+                          f"averaged over its last {COUNTER_STEPS} dispatches (the timed frames) of each --pmc pass; "
+                          "frame = the sum over the frame's kernels (each runs once per frame)",
         }
         summary[c] = ent
-        print(c, json.dumps({k: ent[k] for k in ("kernel_ms", "serial_kernel_ms", "counter_dispatch_ms", "valu_insts",
-                                                  "dram_bytes", "l2_hit", "valu_lane_util", "clock_ghz_profiled")}))
+        print(c, json.dumps({"frame": frame, "frame_serial": fserial,
+                             "per_kernel": {k: (v["valu_insts"], v["dram_bytes"], v["counter_dispatch_ms"])
+                                            for k, v in kernels.items()}}))
         restate(dst / f"bench_{c}.json", ent)
     cpath.write_text(json.dumps(summary, indent=1) + "\n")
 
@@ -163,19 +201,20 @@ def restate(path: Path, ent: dict):
     rf = line.get("roofline") or {}
     t = line["ms_per_step"] if rf.get("time_basis", "").startswith("wall") else rf.get("launch_ms", line["ms_per_step"])
     t *= 1e-3
+    work = ent["frame"] if rf.get("time_basis", "").startswith("wall") else ent["frame_serial"]
     cand = {
-        "valu": {"achieved": round(ent["valu_insts"] / t / 1e9, 2), "peak": VALU_PEAK_GINST,
+        "valu": {"achieved": round(work["valu_insts"] / t / 1e9, 2), "peak": VALU_PEAK_GINST,
                  "unit": "G VALU wave-instructions/s"},
-        "hbm": {"achieved": round(ent["dram_bytes"] / t / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s"},
+        "hbm": {"achieved": round(work["dram_bytes"] / t / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s"},
     }
     for v in cand.values():
         v["frac"] = round(v["achieved"] / v["peak"], 4)
     bound = max(cand, key=lambda k: cand[k]["frac"])
     rf.update({"bound": bound, **{k: cand[bound][k] for k in ("achieved", "peak", "unit", "frac")},
-               "traffic": ent["dram_bytes"], "candidates": cand,
-               "counters": {"source": f"profiles/{path.parent.name}/counters.json", "valu_insts_per_launch": ent["valu_insts"],
-                            "dram_bytes_per_launch": ent["dram_bytes"], "l2_hit": ent["l2_hit"],
-                            "profiled_kernel_ms": ent["kernel_ms"]},
+               "traffic": work["dram_bytes"], "candidates": cand,
+               "counters": {"source": f"profiles/{path.parent.name}/counters.json", "kernels": work["kernels"],
+                            "valu_insts_per_frame": work["valu_insts"], "dram_bytes_per_frame": work["dram_bytes"],
+                            "l2_hit": ent["l2_hit"], "profiled_kernel_ms": ent["kernel_ms"]},
                "restated_from_counters_of_this_run": True})
     line["roofline"] = rf
     path.write_text(json.dumps(line) + "\n")
