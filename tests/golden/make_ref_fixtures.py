@@ -11,6 +11,9 @@ from /root/reference) and runs it on the inputs of tests/ref_scenes.py:
   ref/hdrcache_<env>.json      sha256 of calculateHdrCache's output for the
                                repository's decode of the shipped .hdr, and 4096
                                sampled texels of it
+  ref/hdr_decode_<env>.json    sha256 of the shipped .hdr decoded by the reference's
+                               hdrloader.cpp (oracle/ref_hdr.cpp), its shape and 4096
+                               sampled texels of it
   basic/ref_s<N>.json, .png    the reference CPU tracer (BasicRayTracingWithC++/main.cpp,
                                oracle/ref_basic.cpp) at SAMPLE = N, std::mt19937 seeded
                                5489: sha256 of its double image, 4096 sampled pixels
@@ -115,6 +118,20 @@ def main():
                 ent["tris_f32_zlib_b64"] = pack(tris)
             (OUT / f"{name}_{builder}.json").write_text(json.dumps(ent) + "\n")
             print(name, builder, tris.shape, nodes.shape)
+        for env in ref_scenes.HDRS if len(sys.argv) == 1 or "hdr" in sys.argv[1:] else ():
+            out = tmp / "decoded.bin"
+            subprocess.run([str(ref_build.hdr_exe()), str(scenes.HDR_FILES[env]), str(out)], check=True)
+            raw = np.fromfile(out, np.uint8)
+            w, h = (int(x) for x in np.frombuffer(raw[:8].tobytes(), np.int32))
+            dec = np.frombuffer(raw[8:].tobytes(), np.float32).reshape(h, w, 3)
+            rng = np.random.default_rng(12)
+            idx = rng.choice(h * w, 4096, replace=False)
+            (OUT / f"hdr_decode_{env}.json").write_text(json.dumps({
+                "env": env, "file": Path(scenes.HDR_FILES[env]).name, "width": w, "height": h,
+                "decoded_sha256": sha(dec), "sample_index": idx.tolist(),
+                "sample_values": dec.reshape(-1, 3)[idx].tolist(),
+                "generator": "oracle/ref_hdr (reference hdrloader.cpp decrunch / workOnRGBE)"}) + "\n")
+            print("hdr decode", env, w, h)
         for env in ref_scenes.HDRS if len(sys.argv) == 1 else ():
             hdr = np.ascontiguousarray(scenes.load_hdr(scenes.HDR_FILES[env]), np.float32)
             h, w = hdr.shape[:2]

@@ -87,3 +87,17 @@ def test_hdr_cache_equals_reference(env):
     got = cache.reshape(-1, 3)[np.asarray(f["sample_index"])]
     assert np.array_equal(got, np.asarray(f["sample_values"], np.float32))
     assert sha(np.ascontiguousarray(cache, np.float32)) == f["cache_sha256"]
+
+
+@pytest.mark.parametrize("env", ref_scenes.HDRS)
+def test_hdr_decode_equals_reference(env):
+    """The repository's Radiance decoder (csrc/scene.cpp, pt_hdr_decode) gives the texels of the
+    reference's own hdrloader.cpp decoders (OpenglRayTracing/hdrloader.cpp:93-191, decrunch /
+    oldDecrunch / workOnRGBE, compiled from /root/reference: oracle/ref_hdr.cpp) bit for bit on the
+    shipped environment maps."""
+    f = fixture(f"hdr_decode_{env}")
+    hdr = np.ascontiguousarray(scenes.load_hdr(scenes.HDR_FILES[env]), np.float32)
+    assert hdr.shape == (f["height"], f["width"], 3)
+    got = hdr.reshape(-1, 3)[np.asarray(f["sample_index"])]
+    assert np.array_equal(got, np.asarray(f["sample_values"], np.float32))
+    assert sha(hdr) == f["decoded_sha256"]
