@@ -325,9 +325,17 @@ hipError_t renderBlocksPerCU(int integrator, bool cull, bool count, bool wide, i
 // the camera-ray pass: one wave per 8x8 tile of the rank's tiles, results in p.primHit
 constexpr int PRIM_MISS = -1, PRIM_RETRACE = -2, PRIM_TILE = -3;
 hipError_t launchPrimary(const RenderParams& p, hipStream_t s);
-// the path-regeneration kernel (pt_regen.hip); wide: the large-scene variant (WIDE_REGEN_WAVES)
-hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool wide = false);
-hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb);
+// the path-regeneration kernel (pt_regen.hip): the variant and launch shape of a frame
+struct RegenShape {
+  bool wide = false;      // the large-scene variant (WIDE_REGEN_WAVES, 4-wide walk, dynamic ray fetch)
+  bool fullTree = false;  // ... with the whole 4-wide tree in LDS (small trees, uniform integrators)
+  int block = BLOCK;      // threads per block
+  int blocksPerCU = 0;    // resident blocks per CU
+  size_t dynLds = 0;      // dynamic LDS bytes per block (the tree)
+};
+// f4nDev: nodes of the 4-wide runtime tree the frame walks (0: it walks none)
+hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenShape* out);
+hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, const RegenShape& r);
 int regenLdsStack();
 int regenTop4(int integrator);  // 4-wide nodes the wide regen kernel stages in LDS (PT_REGEN_TOP4[_3])
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);

@@ -252,27 +252,37 @@ __device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int
 // WAVES > 0: compiled for that many waves per SIMD (large scenes, pt_runtime.cpp renderOne).
 // W4: rays walk the 4-wide runtime tree when p.scene.fast (pt_trace.h traceRay4), results
 // checked against the uploaded tree and retraced through it on a tie or an unreachable hit.
-template <int INTEG, bool CULL, int WAVES = 0, bool W4 = false>
-__global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U)) void regenKernel(
+// FULL (with W4): the whole 4-wide tree in LDS -- dynamic shared memory, p.scene.f4nTop =
+// every node, swizzled (pt_trace.h loadNode4Lds) -- one block of BS threads (all the waves a CU
+// holds) sharing one copy: a walk's node visits leave the texture data path to the leaf
+// records.
+template <int INTEG, bool CULL, int WAVES = 0, bool W4 = false, int BS = BLOCK, bool FULL = false>
+__global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U)) void regenKernel(
     RenderParams p) {
-  __shared__ int s_stack[REGEN_LDS_STACK * BLOCK];
-  StackT<REGEN_LDS_STACK, BLOCK> st;
+  static_assert(!FULL || W4, "the LDS tree is the 4-wide one");
+  __shared__ int s_stack[REGEN_LDS_STACK * BS];
+  StackT<REGEN_LDS_STACK, BS> st;
   st.lds = s_stack + threadIdx.x;
-  st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * p.ovfDepth : nullptr;
+  st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BS + threadIdx.x) * p.ovfDepth : nullptr;
   st.reset();
-  // the top of the uploaded tree (every ray's first node visits) staged in LDS once per block
+  // the top of the tree (every ray's first node visits) -- or all of it -- staged in LDS once per block
 #if PT_LDS_NODES > 0
   constexpr int TOP4 = regenTop4W(WAVES);
-  constexpr int TOPF4 = (W4 && TOP4 * W4_F4 > LDS_NODES * 4) ? TOP4 * W4_F4 : LDS_NODES * 4;
+  constexpr int TOPF4 = FULL ? 1 : (W4 && TOP4 * W4_F4 > LDS_NODES * 4) ? TOP4 * W4_F4 : LDS_NODES * 4;
   __shared__ float4 s_nodes[TOPF4];
-  {
+  extern __shared__ float4 s_tree[];  // FULL: f4nTop * W4_F4 float4 (launch's dynamic LDS)
+  if (FULL) {
+    const float4* src = p.scene.fbvh4;
+    const int n = p.scene.f4nTop * W4_F4;
+    for (int i = threadIdx.x; i < n; i += BS) s_tree[swz4(i >> 3, i & 7)] = src[i];
+  } else {
     const bool w4 = W4 && p.scene.fast;
     const float4* src = w4 ? p.scene.fbvh4 : p.scene.bvh;
     const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.nTop * 4;  // the staged tree's own record size
-    for (int i = threadIdx.x; i < n; i += BLOCK) s_nodes[i] = src[i];
+    for (int i = threadIdx.x; i < n; i += BS) s_nodes[i] = src[i];
   }
   __syncthreads();
-  const float4* top = s_nodes;
+  const float4* top = FULL ? s_tree : s_nodes;
 #else
   const float4* top = nullptr;
 #endif
@@ -359,8 +369,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
         walk4Begin(p.scene, w, st, C);
         walking = true;
       }
-      walk4Run<CULL, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(p.scene, s.o, s.d, s.kind == K_SHADOW, w, st,
-                                                                       top, PT_REGEN_YIELD);
+      walk4Run<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0), FULL>(p.scene, s.o, s.d, s.kind == K_SHADOW, w,
+                                                                           st, top, PT_REGEN_YIELD);
       if (!walk4Done(w)) continue;  // stopped for the lanes that are done: resumes next iteration
       walking = false;
       t = w.tbest;
@@ -371,15 +381,15 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
       }
     } else if (W4 && p.scene.fast) {
       bool tie = false;
-      const int pos = traceRay4<CULL, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(p.scene, s.o, s.d, t, st, C,
-                                                                                      s.kind == K_SHADOW, top, &tie);
+      const int pos = traceRay4<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0)>(p.scene, s.o, s.d, t, st, C,
+                                                                                   s.kind == K_SHADOW, top, &tie);
       tri = pos >= 0 ? p.scene.fastTri[pos] : -1;
       if (tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t))) {
         C.rays--;  // the same ray, counted once
         tri = traceRay<false, CULL, false>(p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW);
       }
     } else {
-      tri = traceRay<false, CULL, false, StackT<REGEN_LDS_STACK, BLOCK>, (LDS_NODES > 0)>(
+      tri = traceRay<false, CULL, false, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0)>(
           p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW, top);
     }
     V3 color;
@@ -390,7 +400,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   }
 #if PT_WAVE_TRACE
   if (p.waveTrace && lane == 0) {
-    unsigned long long* r = p.waveTrace + 6 * ((size_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
+    unsigned long long* r = p.waveTrace + 6 * ((size_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6));
     r[0] = wStart; r[1] = wall_clock64(); r[2] = wTiles | wLonePix << 32; r[3] = wLastClaim;
     r[4] = wIters; r[5] = wThin;
   }
@@ -398,31 +408,72 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_M
   addRays(p.rayShards, C.rays);
 }
 
+// The FULL variant: the uniform integrators' wide kernel (3 waves per SIMD) as one block of 12
+// waves per CU, the whole tree beside its 16-entry LDS stacks (PT_LDS_TREE = 0: never)
+#ifndef PT_LDS_TREE
+#define PT_LDS_TREE 1
+#endif
+constexpr int FULL_BS = 768;
+constexpr size_t LDS_BYTES = 160 * 1024;
 template <int I>
-static const void* regenFn(bool cull, bool wide) {
+static const void* regenFn(bool cull, bool wide, bool full) {
+  if constexpr (wideRegenWaves(I) == 3)  // the 3-wave (uniform integrators') variant only
+    if (full) return (const void*)regenKernel<I, true, wideRegenWaves(I), true, FULL_BS, true>;
   if (wide) return (const void*)regenKernel<I, true, wideRegenWaves(I), true>;
   return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
 }
+static const void* regenFnI(int integrator, bool cull, bool wide, bool full) {
+  return integrator == 0 ? regenFn<0>(cull, wide, full) : integrator == 1 ? regenFn<1>(cull, wide, full)
+                                                                         : regenFn<2>(cull, wide, full);
+}
+
+hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenShape* out) {
+  RegenShape r;
+  r.wide = wide && cull;
+  const size_t treeBytes = (size_t)f4nDev * W4_F4 * sizeof(float4);
+  const size_t staticBytes = (size_t)REGEN_LDS_STACK * FULL_BS * sizeof(int) + 2 * sizeof(float4);
+  r.fullTree = PT_LDS_TREE && r.wide && integrator != 2 && wideRegenWaves(integrator) == 3 && f4nDev > 0 &&
+               treeBytes + staticBytes <= LDS_BYTES;
+  r.block = r.fullTree ? FULL_BS : BLOCK;
+  r.dynLds = r.fullTree ? treeBytes : 0;
+  const void* f = regenFnI(integrator, cull, r.wide, r.fullTree);
+  if (r.fullTree) {  // once per kernel: room for any tree that fits beside the stacks
+    static bool granted[3] = {false, false, false};
+    if (!granted[integrator]) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BYTES - staticBytes));
+      if (e != hipSuccess) return e;
+      granted[integrator] = true;
+    }
+  }
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&r.blocksPerCU, f, r.block, r.dynLds);
+  *out = r;
+  return e;
+}
+
 template <int I>
-static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, bool wide) {
-  if (wide && cull)
+static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, const RegenShape& r) {
+  if constexpr (wideRegenWaves(I) == 3) {
+    if (r.fullTree) {
+      hipLaunchKernelGGL((regenKernel<I, true, wideRegenWaves(I), true, FULL_BS, true>), dim3(grid), dim3(FULL_BS),
+                         r.dynLds, s, p);
+      return hipGetLastError();
+    }
+  }
+  if (r.fullTree) return hipErrorInvalidValue;
+  if (r.wide)
     hipLaunchKernelGGL((regenKernel<I, true, wideRegenWaves(I), true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else hipLaunchKernelGGL((regenKernel<I, false>), dim3(grid), dim3(BLOCK), 0, s, p);
   return hipGetLastError();
 }
 
-hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool wide) {
+hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, const RegenShape& r) {
+  if (r.fullTree && p.scene.f4nTop * W4_F4 * sizeof(float4) > r.dynLds) return hipErrorInvalidValue;
   switch (integrator) {
-    case 0: return launchRegenI<0>(p, grid, s, cull, wide);
-    case 1: return launchRegenI<1>(p, grid, s, cull, wide);
-    default: return launchRegenI<2>(p, grid, s, cull, wide);
+    case 0: return launchRegenI<0>(p, grid, s, cull, r);
+    case 1: return launchRegenI<1>(p, grid, s, cull, r);
+    default: return launchRegenI<2>(p, grid, s, cull, r);
   }
-}
-
-hipError_t regenBlocksPerCU(int integrator, bool cull, bool wide, int* nb) {
-  const void* f = integrator == 0 ? regenFn<0>(cull, wide) : integrator == 1 ? regenFn<1>(cull, wide) : regenFn<2>(cull, wide);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, f, BLOCK, 0);
 }
 
 int regenLdsStack() { return REGEN_LDS_STACK; }

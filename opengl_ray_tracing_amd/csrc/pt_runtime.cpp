@@ -1588,13 +1588,20 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     return PT_OK;
   };
   int nb = 0;
-  // the more-waves variant of either kernel (PT_REGEN_WIDE=1: the regen kernel's on any scene,
-  // with its 4-wide walk, dynamic ray fetch and camera-ray pass)
+  // the more-waves variant of either kernel (the regen kernel's with its 4-wide walk, dynamic ray
+  // fetch and camera-ray pass; on small trees with the whole tree in LDS)
   const bool wide = wideScene || (regen && regenAll);
-  if (regen) CK(regenBlocksPerCU(c.integrator, cull, wide, &nb));
-  else CK(renderBlocksPerCU(c.integrator, cull, count, wide, &nb));
+  const bool walk4 = wide && ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE);
+  RegenShape rs;
+  if (regen) {
+    CK(regenShape(c.integrator, cull, wide, walk4 ? ctx->f4nDev : 0, &rs));
+    nb = rs.blocksPerCU;
+  } else {
+    CK(renderBlocksPerCU(c.integrator, cull, count, wide, &nb));
+  }
   if (nb < 1) nb = 1;
-  ctx->lastWaves = nb * BLOCK / 64 / 4;  // 4 SIMDs per CU
+  const int bs = regen ? rs.block : BLOCK;  // threads per block
+  ctx->lastWaves = nb * bs / 64 / 4;  // 4 SIMDs per CU
   ctx->lastRegen = regen;
   // Frames in flight share the GPU by space, not by time: a frame's persistent grid is
   // residency / (frames in flight), so the frames' waves are all resident together and a
@@ -1618,7 +1625,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     if (others) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * D)));
   }
   int ovfDepth = 0;
-  int rc = ensureOverflow(ctx, (size_t)fullGrid * BLOCK, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
+  int rc = ensureOverflow(ctx, (size_t)fullGrid * bs, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
   if (rc) return rc;
   const size_t npix = (size_t)c.width * c.height;
   // the colour buffer's previous launch (nCol back) has been mixed (the slot's queue counters,
@@ -1649,7 +1656,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.shardsX = ctx->shardsX;
   p.rank = c.tile_rank;
   p.world = c.tile_world;
-  p.ovf = ovfDepth ? ctx->d_ovf + (size_t)slot * fullGrid * BLOCK * ovfDepth : nullptr;
+  p.ovf = ovfDepth ? ctx->d_ovf + (size_t)slot * fullGrid * bs * ovfDepth : nullptr;
   p.ovfDepth = ovfDepth;
   p.scene.fast = 0;  // probePolicy below
 
@@ -1681,8 +1688,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
                                    !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast,
                                    &noOrder);
   // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
-  if (regen && wide && ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE)) useFast = true;
-  if (regen && wide) p.scene.f4nTop = std::min(regenTop4(c.integrator), ctx->f4nDev);  // its own LDS copy's size
+  if (regen && walk4) useFast = true;
+  if (regen && wide)  // its own LDS copy's size: the top of the tree, or all of it
+    p.scene.f4nTop = rs.fullTree ? ctx->f4nDev : std::min(regenTop4(c.integrator), ctx->f4nDev);
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   // While the policy probe times frames (PT_SPLIT_AUTO, 20 frames after a restart) a pipelined
@@ -1770,7 +1778,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // diagnostics build: each wave's {start, end, tiles | longest tile's pixel << 32,
   // longest tile's duration, its most node-loop / leaf-loop iterations of a lane} (100 MHz wall
   // clock), appended per frame to $PT_WAVE_TRACE_FILE (tools/wave_trace.py)
-  const size_t nTrace = (size_t)grid * (BLOCK / 64) * 6;
+  const size_t nTrace = (size_t)grid * (bs / 64) * 6;
   unsigned long long* dTrace = nullptr;
   {
     CK(hipMalloc(&dTrace, nTrace * sizeof(unsigned long long)));
@@ -1783,7 +1791,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (!p.primHit) CK(hipMemsetAsync(queue, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), S));
   CK(hipEventRecord(evb, S));
   if (p.primHit) CK(launchPrimary(p, S));
-  if (regen) CK(launchRegen(p, c.integrator, grid, S, cull, wide));
+  if (regen) CK(launchRegen(p, c.integrator, grid, S, cull, rs));
   else CK(launchRender(p, c.integrator, grid, S, cull, count, wide));
 #if PT_WAVE_TRACE
   if (dTrace) {

@@ -377,6 +377,17 @@ __device__ __forceinline__ void loadNode4(const float4* nd, float4& lx, float4& 
                                           float4& hz, float4& rf) {
   lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
 }
+// The whole 4-wide tree in LDS (the regen kernel's FULL variant): node k's float4 j is stored
+// at 8k + ((j + k) & 7). Lanes of a wave read different nodes; unrotated, the j-th float4 of
+// every node would sit in the same 4 of LDS's 64 banks (records are 128 B) and a
+// ds_read_b128 of 16 lanes would serialise on them; rotating by the node id spreads them
+// over all 16 bank quads.
+__device__ __forceinline__ int swz4(int k, int j) { return 8 * k + ((j + k) & 7); }
+__device__ __forceinline__ void loadNode4Lds(const float4* tree, int k, float4& lx, float4& ly, float4& lz, float4& hx,
+                                             float4& hy, float4& hz, float4& rf) {
+  lx = tree[swz4(k, 0)], ly = tree[swz4(k, 1)], lz = tree[swz4(k, 2)], hx = tree[swz4(k, 3)];
+  hy = tree[swz4(k, 4)], hz = tree[swz4(k, 5)], rf = tree[swz4(k, 6)];
+}
 template <bool CULL, class StackType, bool LDSTOP>
 __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& tOut, StackType& st, Counters& C,
                                          bool anyRT, const float4* top, bool* tie) {
@@ -509,7 +520,8 @@ __device__ __forceinline__ void walk4Begin(const SceneView& S, Walk4& w, StackTy
   st.reset();
   C.rays++;
 }
-template <bool CULL, class StackType, bool LDSTOP>
+// ALL: every node is in LDS at `top`, swizzled (loadNode4Lds); else the first S.f4nTop are, in order
+template <bool CULL, class StackType, bool LDSTOP, bool ALL = false>
 __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool anyRT, Walk4& w, StackType& st,
                                          const float4* top, int yield) {
   const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -521,10 +533,14 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
     if (__ballot(!done) == 0 || __popcll(__ballot(done)) >= yield) break;  // wave-uniform
     if (done) continue;
     while (w.ref >= 0) {
-      const float4* nd = S.fbvh4 + (size_t)W4_F4 * w.ref;
-      if (LDSTOP && w.ref < S.f4nTop) nd = top + W4_F4 * w.ref;
       float4 lx, ly, lz, hx, hy, hz, rf;
-      loadNode4(nd, lx, ly, lz, hx, hy, hz, rf);
+      if (ALL) {
+        loadNode4Lds(top, w.ref, lx, ly, lz, hx, hy, hz, rf);
+      } else {
+        const float4* nd = S.fbvh4 + (size_t)W4_F4 * w.ref;
+        if (LDSTOP && w.ref < S.f4nTop) nd = top + W4_F4 * w.ref;
+        loadNode4(nd, lx, ly, lz, hx, hy, hz, rf);
+      }
       float key[4];
       int r[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
       const float lim = w.tbest + 1e-3f * fmaxf(1.0f, w.tbest);
