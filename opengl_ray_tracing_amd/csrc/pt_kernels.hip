@@ -91,6 +91,23 @@ struct Tracer {
     // COUNT reproduces the reference's closest-hit shadow query fetch by fetch
     return traceRay<!COUNT, CULL, COUNT, Stack, (LDS_NODES > 0)>(S, o, d, t, st, C, false, top) >= 0;
   }
+  // closest (anyhit false) or env-shadow (anyhit true: >= 0 = occluded) query through ONE call site
+  // of the traversal, so a path loop that traces its shadow and BRDF rays from the same place
+  // keeps one copy of the walk (and its registers) live: trace() / occluded() per lane
+  __device__ __forceinline__ int traceK(V3 o, V3 d, bool anyhit, float& t) {
+    if (PT_WIDE4 && !COUNT && S.fast) {
+      bool tie = false;
+      const int pos = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, anyhit, top, &tie);
+      int tri = pos >= 0 ? S.fastTri[pos] : -1;
+      if ((tie && !anyhit) || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
+        C.rays--;  // the same ray, counted once
+        tri = traceRay<false, CULL, false, Stack>(S, o, d, t, st, C, anyhit);
+      }
+      return tri;
+    }
+    if (anyhit) return occluded(o, d) ? 0 : -1;
+    return trace(o, d, t);
+  }
 };
 
 // pathTracing O:329-364
@@ -155,14 +172,17 @@ __device__ V3 pathDisneyUniform(T& tr, const Env& env, Hit hit, int maxBounce, u
 // material -- the light sample's contribution and the BRDF sample with its
 // f_r and pdf -- is computed before either ray of the bounce is traced, and
 // the light contribution is added only if the shadow ray is unoccluded. No
-// material, view vector or normal is live across a traversal, which keeps the
-// kernel's register peak near the traversal's own. Random numbers are drawn
-// in the reference's order (r1, r2, then xi_3); the shadow ray is traced and
-// counted exactly when the reference traces it.
+// material, view vector or normal is live across a traversal. Random numbers are
+// drawn in the reference's order (r1, r2, then xi_3); the shadow ray is traced and
+// counted exactly when the reference traces it. Both rays of a bounce go through
+// one traversal call site (Tracer::traceK): the loop's phase says which ray is in
+// flight, so a lane whose bounce has no shadow ray walks its BRDF ray beside
+// another lane's shadow ray, and the kernel holds one copy of the walk.
 template <class T>
 __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& seed, int px, int py,
                       uint32_t frameCounter, Counters& C, bool count) {
   V3 Lo = v3(0, 0, 0), history = v3(1, 1, 1);
+  if (maxBounce <= 0) return Lo;
   const uint32_t gi = grayCode(frameCounter + 1u);  // frameCounter = the sample index here
   float cpu, cpv;
   cranleyPattersonShift(px, py, cpu, cpv);
@@ -180,10 +200,10 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
       V3 color;
       float pdf_light;
       hdrColorPdf(env, Ldir, color, pdf_light);
-      V3 f_r = brdfIso(V, N, Ldir, hit.m);
-      float pdf_brdf = brdfPdf(V, N, Ldir, hit.m);
-      float mis_weight = misWeight(pdf_light, pdf_brdf);
-      V3 c = ((history * mis_weight) * color) * f_r;
+      const V3 fl = brdfIso(V, N, Ldir, hit.m);
+      const float pb = brdfPdf(V, N, Ldir, hit.m);
+      const float mis_weight = misWeight(pdf_light, pb);
+      const V3 c = ((history * mis_weight) * color) * fl;
       lightC = (c * dot(N, Ldir)) / pdf_light;
     }
     // (2) BRDF sample IS:791-840
@@ -195,27 +215,40 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
     const float NdotL = dot(N, L);
     const V3 f_r = brdfIso(V, N, L, hit.m);
     const float pdf_brdf = brdfPdf(V, N, L, hit.m);
-    if (tryLight && !tr.occluded(hit.P, Ldir)) {
-      Lo = Lo + lightC;
-      if (count) C.texels += 2;
+    const V3 P = hit.P;
+    if (!tryLight && NdotL <= 0.0f) break;  // IS:818: no ray left in this bounce
+    // (3) the bounce's rays, the env shadow ray first when there is one, through one call site
+    bool shadow = tryLight, end = false;
+    int tri;
+    float t;
+    while (true) {
+      tri = tr.traceK(P, shadow ? Ldir : L, shadow, t);
+      if (!shadow) break;
+      if (tri < 0) {  // IS:776-790
+        Lo = Lo + lightC;
+        if (count) C.texels += 2;
+      }
+      shadow = false;
+      if (NdotL <= 0.0f) {
+        end = true;
+        break;
+      }
     }
-    if (NdotL <= 0.0f) break;
-    Hit nh;
-    bool isHit = tr.closest(hit.P, L, nh);
-    if (pdf_brdf <= 0.0f) break;
-    if (!isHit) {
+    if (end) break;
+    if (pdf_brdf <= 0.0f) break;  // IS:816: the ray is traced, then discarded
+    if (tri < 0) {  // IS:819-829
       V3 color;
       float pdf_light;
       hdrColorPdf(env, L, color, pdf_light);
       if (count) C.texels += 2;
-      float mis_weight = misWeight(pdf_brdf, pdf_light);
-      V3 c = ((history * mis_weight) * color) * f_r;
+      const float mis_weight = misWeight(pdf_brdf, pdf_light);
+      const V3 c = ((history * mis_weight) * color) * f_r;
       Lo = Lo + (c * NdotL) / pdf_brdf;
       break;
     }
-    V3 Le = nh.m.emissive;
+    finishHit(tr.S, tri, P, L, t, hit);  // IS:831-840: the next bounce's hit
+    const V3 Le = hit.m.emissive;
     Lo = Lo + ((history * Le) * f_r * NdotL) / pdf_brdf;
-    hit = nh;
     history = history * ((f_r * NdotL) / pdf_brdf);
   }
   return Lo;
