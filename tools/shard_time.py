@@ -14,9 +14,12 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
+# the bench's hardware queues (bench.py): 12, so the frames in flight get a queue each
 import os  # noqa: E402
+if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 12:
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
 
-import opengl_ray_tracing_amd  # noqa: E402,F401  (raises GPU_MAX_HW_QUEUES before HIP initialises)
+import opengl_ray_tracing_amd  # noqa: E402,F401
 
 
 def main():

@@ -21,6 +21,10 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
+# the bench's hardware queues (bench.py): 12, so the frames in flight get a queue each
+import os  # noqa: E402
+if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 12:
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
 
 
 def child(variant: str, config: str, frames: int, warmup: int, builder, flags: int = 0, max_bounce=None):
