@@ -2,10 +2,10 @@
 """Per-rank frame time of the screen-tile split, measured on one GPU: rank 0's
 share of an N-way split (its 32x32 tiles t % N == 0) rendered alone, wall ms per
 frame with frames in flight and frames batched per launch (pt_render_frames_async,
-PT_BATCH frames per launch, 0 = the renderer's choice: N). The N-GPU frame is at
+PT_BATCH frames per launch, 0 = the renderer's choice; PT_BATCH_MUL = m: m x N). The N-GPU frame is at
 least this plus whatever of the per-batch gather does not overlap the next batch.
 
-    [PT_VARIANT=<tuning build>] [PT_BATCH=b] python tools/shard_time.py [config] [N ...]
+    [PT_VARIANT=<tuning build>] [PT_BATCH=b | PT_BATCH_MUL=m] python tools/shard_time.py [config] [N ...]
 """
 import json
 import sys
@@ -35,9 +35,10 @@ def main():
     cfg, tris, nodes, hdr = scenes.build_config(cfg_name)
     eye, rot = orbit_camera(*cfg.camera)
     batch = int(os.environ.get("PT_BATCH", "0"))
+    mul = int(os.environ.get("PT_BATCH_MUL", "0"))  # frames per launch = mul x N (overrides PT_BATCH)
     for n in worlds:
         with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, tile_rank=0,
-                      tile_world=n, frame_batch=batch) as r:
+                      tile_world=n, frame_batch=mul * n if mul else batch) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
             r.render_frames(eye, rot, 0, 100)  # policy probe (tree, split, order) + warmup
