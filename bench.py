@@ -9,8 +9,8 @@ OpenglRayTracing bunny scene (5k tris) at 1920x1080, Lambert, 2 bounces.
 N > 1 ranks (one process per GPU):
   --shard tiles (default, strong scaling: BASELINE north_star's split): every
       rank renders its 32x32 screen tiles of the one frame, in batches of
-      tile_world frames per launch (pt_render_frames_async: each frame 1 spp and
-      its own running-mean update, about one whole image's work per launch);
+      2 x tile_world frames per launch (pt_render_frames_async: each frame 1 spp and
+      its own running-mean update, about two whole images' work per launch);
       after every batch the running means of the rank's pixels (f32 radiance,
       12 B/pixel) are gathered to rank 0 over RCCL (bit-exact reassembly),
       pipelined one batch deep: batch b's gather runs on a communication stream
@@ -85,7 +85,8 @@ def parse():
                          "3 f32 per pixel) or the displayed frame (RGB8, 3 B/pixel; the running means then "
                          "gathered once after the run)")
     ap.add_argument("--batch", type=int, default=0,
-                    help="frames per launch (pt_config.frame_batch; 0 = the renderer's choice: tile_world)")
+                    help="frames per launch (pt_config.frame_batch; 0 = the renderer's choice: 2 x tile_world, "
+                         "tile_world on large Disney/MIS scenes)")
     ap.add_argument("--shard", choices=["samples", "tiles"], default="tiles",
                     help="N > 1: sample-parallel full frames (weak) or screen-tile shards of one frame (strong)")
     return ap.parse_args()

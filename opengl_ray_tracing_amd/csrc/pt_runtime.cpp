@@ -283,6 +283,17 @@ int pt_device_count(int* n) {
 
 const char* pt_last_error(pt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
+// Frames per launch of pt_render_frames_async: pt_config.frame_batch, else two whole images' work
+// per launch (2 x tile_world frames) -- one image's is enough to fill the machine, the second
+// halves the launches and running-mean updates per frame: c2 0.244 -> 0.231 ms per frame at N = 1,
+// c4 0.326 -> 0.318, c2's 1/8 share 0.0354 -> 0.0344, c4's 0.0477 -> 0.0446 (profiles/r4) -- and
+// one image's on large Disney/MIS scenes (c5 5.66 ms at 1, 5.86 at 2 frames per launch).
+static int batchFor(const pt_ctx* ctx, bool wideScene) {
+  const pt_config& c = ctx->cfg;
+  if (c.frame_batch > 0) return std::min(c.frame_batch, MAX_BATCH);
+  return std::max(1, std::min((wideScene ? 1 : 2) * std::max(1, c.tile_world), MAX_BATCH));
+}
+
 static int createOne(pt_ctx** out, const pt_config* cfg) {
   if (!out || !cfg) return PT_E_INVALID;
   *out = nullptr;
@@ -369,8 +380,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
       ctx->pipeDepthFixed = true;
     }
     ctx->pipeDepthBase = ctx->pipeDepth;
-    ctx->batchCap = cfg->frame_batch > 0 ? std::min(cfg->frame_batch, MAX_BATCH)
-                                         : std::max(1, std::min(cfg->tile_world, MAX_BATCH));
+    ctx->batchCap = batchFor(ctx, false);
     // slot streams are created as a depth first uses them (ensureSlots): streams beyond the
     // hardware queues share queues, which serialises their work
     for (int k = 0; k < COLS; k++) CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
@@ -891,6 +901,10 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
     const bool wideScene = ctx->cfg.integrator != 0 && !(ctx->cfg.flags & PT_FLAG_NO_CULL) &&
                            sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
     ctx->pipeDepth = wideScene ? std::min(ctx->pipeDepthBase, 4) : ctx->pipeDepthBase;
+  }
+  if (ctx->pipe) {
+    const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + HIT_F4 * 16) + (size_t)ctx->nDevNodes * 64;
+    ctx->batchCap = batchFor(ctx, ctx->cfg.integrator != 0 && sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20));
   }
   ctx->rootRef = h.ref.rootRef;
   ctx->depth = h.ref.depth;

@@ -85,7 +85,8 @@ class Renderer:
         """devices: a list of HIP device ids (2..8, repeats allowed) makes this one context render
         screen tiles on all of them and gather them into the first device's accumulation every
         frame (pt_config.n_devices; gather "auto" / "copy" / "rccl"). frame_batch: most frames per
-        launch of render_frames (0 = automatic: tile_world frames of a screen-tile share)."""
+        launch of render_frames (0 = automatic: 2 x tile_world frames; tile_world on large Disney/MIS
+        scenes)."""
         self._lib = _native.load()
         cfg = _native.PtConfig()
         cfg.width, cfg.height = int(width), int(height)
