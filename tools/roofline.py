@@ -18,7 +18,8 @@ longest-first order) and the running-mean update mixKernel. The profiled bench r
 timed frames (--no-reset --no-serial --no-psnr), so each kernel's last K dispatches are the timed
 frames' (K = the run's --steps).
 
-Per kernel (averaged over its timed dispatches of each pass) and summed per frame:
+Per kernel (averaged over its timed dispatches of each pass, divided by the frames a dispatch
+renders: the bench's frames_per_launch) and summed per frame:
   valu_insts = SQ_INSTS_VALU (wave64 instructions; peak issue 1024 SIMDs x 2.4 GHz / 2 cycles)
   dram_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   (KiB units; gfx950 FETCH_SIZE halving)
   l2_hit     = TCC_HIT / (TCC_HIT + TCC_MISS)
@@ -88,8 +89,13 @@ def main():
         d = dst / c
         d.mkdir(exist_ok=True)
         shutil.copy(one(f"{prof}/trace/**/run_kernel_stats.csv"), d / "kernel_stats.csv")
+        # frames per launch of the profiled bench (pt_render_frames_async batches): each frame kernel's
+        # dispatch covers F frames, so the timed frames are the last steps / F dispatches and a
+        # dispatch's work is F frames' work
+        bl = [ln for ln in (prof / "bench_line.json").read_text().splitlines() if ln.startswith("{")]
+        F = int(json.loads(bl[-1])["config"].get("frames_per_launch") or 1) if bl else 1
         trace = list(csv.DictReader(open(one(f"{prof}/trace/**/run_kernel_trace.csv"))))
-        sel = last_dispatches(trace, TRACE_STEPS)
+        sel = last_dispatches(trace, max(1, TRACE_STEPS // F))
         serial = {}
         sp = sorted(glob.glob(f"{prof}/serial/**/run_kernel_trace.csv", recursive=True))
         if sp:
@@ -98,7 +104,7 @@ def main():
         disp = {}
         for kd, rows in sel.items():
             ms = [dur_ms(r) for r in rows]
-            disp[kd] = {"kernel": rows[-1]["Kernel_Name"], "timed_dispatches": len(rows),
+            disp[kd] = {"kernel": rows[-1]["Kernel_Name"], "timed_dispatches": len(rows), "frames_per_dispatch": F,
                         "avg_ms_pipelined": round(sum(ms) / len(ms), 4), "min_ms_pipelined": round(min(ms), 4),
                         "vgpr": rows[-1].get("VGPR_Count"), "scratch": rows[-1].get("Scratch_Size")}
             if kd in serial:
@@ -126,7 +132,7 @@ def main():
             for di in sorted(by_disp, key=int):
                 per_kind[kind_of(by_disp[di][0]["Kernel_Name"])].append(di)
             for kd, dis in per_kind.items():
-                for di in dis[-COUNTER_STEPS:]:
+                for di in dis[-max(1, COUNTER_STEPS // F):]:
                     for r in by_disp[di]:
                         vals[kd][r["Counter_Name"]].append(float(r["Counter_Value"]))
                         rows_out.append({"pass": name, **r})
@@ -141,7 +147,8 @@ def main():
         for kd, v in vals.items():
             if not v:
                 continue
-            m = {k: sum(x) / len(x) for k, x in v.items()}
+            # per frame: a dispatch's counters over the F frames it rendered (time keys stay per dispatch)
+            m = {k: sum(x) / len(x) / (1 if k.startswith("_") else F) for k, x in v.items()}
             g = lambda k: m.get(k, float("nan"))  # noqa: E731
             kernels[kd] = {
                 "kernel": disp.get(kd, {}).get("kernel"),
@@ -149,7 +156,7 @@ def main():
                 "dram_bytes": round((2 * g("FETCH_SIZE") + g("WRITE_SIZE")) * 1024),
                 "l2_hit": round(g("TCC_HIT_sum") / max(g("TCC_HIT_sum") + g("TCC_MISS_sum"), 1.0), 4),
                 "valu_lane_util": round(g("SQ_THREAD_CYCLES_VALU") / max(64 * g("SQ_ACTIVE_INST_VALU"), 1.0), 4),
-                "counter_dispatch_ms": round(g("_dispatch_ms"), 4),
+                "counter_dispatch_ms": round(g("_dispatch_ms") / F, 4),  # per frame
                 "avg_ms_serial": disp.get(kd, {}).get("avg_ms_serial"),
                 "avg_ms_pipelined": disp.get(kd, {}).get("avg_ms_pipelined"),
                 "counters_per_launch": {k: round(x, 1) for k, x in sorted(m.items()) if not k.startswith("_")},
@@ -173,6 +180,7 @@ def main():
             "serial_kernel_ms": disp.get("frame", {}).get("avg_ms_serial"),
             # ... and every kernel of a frame
             "kernels": kernels,
+            "frames_per_launch": F,
             "frame": frame,            # all frame kernels: work over bench.py's wall ms per frame
             "frame_serial": fserial,   # without mixKernel: work over the serial frames' kernel time
             "derivation": "per kernel: valu_insts = SQ_INSTS_VALU; dram_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024, "
