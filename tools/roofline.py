@@ -44,7 +44,7 @@ TRACE_STEPS = 30    # tools/gpu_profile.sh: --steps 30 under --kernel-trace (pip
 COUNTER_STEPS = 10  # --steps 10 under each --pmc pass
 FRAME_KERNELS = {
     "primary": re.compile(r"primaryKernel"),
-    "frame": re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true(, \d+)?(, (true|false))?>"),
+    "frame": re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true[^>]*>"),
     "reorder": re.compile(r"reorderKernel"),
     "mix": re.compile(r"mixKernel"),
 }
