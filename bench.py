@@ -25,10 +25,12 @@ N > 1 ranks (one process per GPU):
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver launch for N > 1)
 
 Rank 0 prints one JSON line (contract in the task statement), with
-``roofline`` for the frame kernel: the per-launch work the hardware counters
-measured for it (VALU wave-instructions, DRAM-side bytes; committed under
-profiles/r3/counters.json by tools/roofline.py) over its live HIP-event
-duration, against each resource's peak -- ``bound`` is the resource with the
+``roofline`` for a frame: the work the hardware counters measured for every kernel
+of a frame (camera-ray pass, frame kernel, tile reorder, running-mean update: VALU
+wave-instructions, DRAM-side bytes; committed under profiles/r4/counters.json by
+tools/roofline.py) over this run's live wall time per frame (and, as kernel_basis,
+over the serially issued frames' HIP-event time), against each resource's peak --
+``bound`` is the resource with the
 highest fraction -- plus ``equivalent_GBs``, the reference algorithm's fetch
 bytes per launch over the same duration; and ``cpu_baseline``
 (the CPU restatement of the reference on the host cores, rank 0 at N = 1).
