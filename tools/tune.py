@@ -38,13 +38,11 @@ def child(variant: str, config: str, frames: int, warmup: int, builder, flags: i
     with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=mb, flags=flags) as r:
         r.upload_scene(tris, nodes)
         r.upload_env(hdr)
-        for f in range(warmup):
-            r.render_frame(eye, rot, f, sync=False)
+        r.render_frames(eye, rot, 0, warmup)  # as bench.py: the renderer's frames per launch
         r.synchronize()
         r.reset_stats()
         t0 = time.perf_counter()
-        for f in range(frames):
-            r.render_frame(eye, rot, warmup + f, sync=False)
+        r.render_frames(eye, rot, warmup, frames)
         r.synchronize()
         wall = (time.perf_counter() - t0) * 1e3 / frames
         st = r.stats()
@@ -52,7 +50,7 @@ def child(variant: str, config: str, frames: int, warmup: int, builder, flags: i
     # frames in flight overlap their launches: wall ms per frame is the comparable figure
     print(json.dumps({"variant": variant, "flags": flags, "config": config, "max_bounce": mb, "kernel_ms": round(ms, 4),
                       "wall_ms": round(wall, 4),
-                      "rays": st.rays // max(st.launches, 1),
+                      "rays": st.rays // max(st.frames, 1), "frames_per_launch": st.frame_batch,
                       "mrays_s": round(st.rays / (st.kernel_ms_total * 1e-3) / 1e6, 1)}), flush=True)
 
 
