@@ -45,6 +45,12 @@ constexpr int wideRegenWaves(int integrator) { return integrator == 2 ? PT_WIDE_
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
+// the MIS megakernel at 3 waves per SIMD (168 VGPRs; 208 uncapped, so ~30 spill): c4 0.321 ->
+// 0.291 ms per frame (tools/tune.py, 3 rounds; round 3's kernel, 231 VGPRs with 142 spilled at 3
+// waves, had measured no gain)
+#ifndef PT_MIN_WAVES_MIS
+#define PT_MIN_WAVES_MIS 3
+#endif
 constexpr int LDS_STACK = PT_LDS_STACK;
 #ifndef PT_LDS_NODES
 #define PT_LDS_NODES 128

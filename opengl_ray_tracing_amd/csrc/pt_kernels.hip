@@ -854,7 +854,9 @@ __device__ __forceinline__ uint32_t waveSum(uint32_t v) {
 // WAVES > 0: compiled for that many waves per SIMD (the latency-bound large
 // scenes' variant, pt_runtime.cpp renderFrame)
 template <int INTEG, bool CULL, bool COUNT, int WAVES = 0>
-__global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES : (INTEG == 0 ? PT_MIN_WAVES_LAMBERT : PT_MIN_WAVES)) void renderKernel(
+__global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
+                                             : (INTEG == 0 ? PT_MIN_WAVES_LAMBERT
+                                                           : INTEG == 2 ? PT_MIN_WAVES_MIS : PT_MIN_WAVES)) void renderKernel(
     RenderParams p) {
   __shared__ int s_stack[LDS_STACK * BLOCK];
   Stack st;
