@@ -189,7 +189,11 @@ __device__ __forceinline__ bool continueFromHit(const RenderParams& p, PathState
 }
 
 // Advance the path by the result (tri, t) of its ray in flight. Returns false
-// when the path has ended (its final color in `color`).
+// when the path has ended (its final color in `color`). A camera ray's hit and a
+// bounce ray's hit go through ONE finishHit and ONE continueFromHit (the same
+// operations on the same values as separate paths would make): the lanes of a wave
+// holding either kind shade together, and the kernel keeps one copy of the
+// shading code.
 template <int INTEG>
 __device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int tri, float t, V3& color) {
   const SceneView& S = p.scene;
@@ -203,48 +207,38 @@ __device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int
     s.kind = K_BOUNCE;
     return true;
   }
-  Hit hit;
-  if (s.kind == K_PRIMARY) {
-    if (tri < 0) {  // IS:857-859
+  const bool primary = s.kind == K_PRIMARY;
+  if (tri < 0) {
+    if (primary) {  // IS:857-859
       color = sampleHdr(p.env, s.d);
       return false;
     }
-    finishHit(S, tri, s.o, s.d, t, hit);
-    s.Le0 = hit.m.emissive;
-    if (continueFromHit<INTEG>(p, s, hit, 0)) return true;
-    color = s.Le0 + s.Lo;
-    return false;
-  }
-  // K_BOUNCE
-  if (INTEG == 2) {
-    if (tri < 0) {  // IS:819-829
+    if (INTEG == 2) {  // IS:819-829
       V3 c;
       float pdf_light;
       hdrColorPdf(p.env, s.d, c, pdf_light);
       float mis_weight = misWeight(s.pdfB, pdf_light);
       V3 cc = ((s.hist * mis_weight) * c) * s.f_r;
       s.Lo = s.Lo + (cc * s.cosL) / s.pdfB;
-      color = s.Le0 + s.Lo;
-      return false;
-    }
-    finishHit(S, tri, s.o, s.d, t, hit);  // IS:833-837
-    V3 Le = hit.m.emissive;
-    s.Lo = s.Lo + ((s.hist * Le) * s.f_r * s.cosL) / s.pdfB;
-    s.hist = s.hist * ((s.f_r * s.cosL) / s.pdfB);
-  } else {  // O:347-360 / D:463-479
-    const float pdf = 1.0f / (2.0f * PT_PI);
-    if (tri < 0) {
+    } else {  // O:347-360 / D:463-479
+      const float pdf = 1.0f / (2.0f * PT_PI);
       V3 sky = sampleHdr(p.env, s.d);
       s.Lo = s.Lo + ((s.hist * sky) * s.f_r * s.cosL) / pdf;
-      color = s.Le0 + s.Lo;
-      return false;
     }
-    finishHit(S, tri, s.o, s.d, t, hit);
-    V3 Le = hit.m.emissive;
+    color = s.Le0 + s.Lo;
+    return false;
+  }
+  Hit hit;
+  finishHit(S, tri, s.o, s.d, t, hit);  // IS:833-837 (a bounce), IS:852-856 (the camera ray)
+  const V3 Le = hit.m.emissive;
+  if (primary) {
+    s.Le0 = Le;
+  } else {
+    const float pdf = INTEG == 2 ? s.pdfB : 1.0f / (2.0f * PT_PI);
     s.Lo = s.Lo + ((s.hist * Le) * s.f_r * s.cosL) / pdf;
     s.hist = s.hist * ((s.f_r * s.cosL) / pdf);
   }
-  if (continueFromHit<INTEG>(p, s, hit, s.bounce + 1)) return true;
+  if (continueFromHit<INTEG>(p, s, hit, primary ? 0 : s.bounce + 1)) return true;
   color = s.Le0 + s.Lo;
   return false;
 }
@@ -297,6 +291,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
   bool active = false;
   bool walking = false;  // PT_REGEN_YIELD: the lane's ray has a walk in progress (w, st)
+  int pendTri = -1;      // >= 0: the camera ray's result from the camera-ray pass, not yet shaded
+  float pendT = 0.0f;
   Walk4 w;
   PathState s;
   s.px = s.py = s.fr = 0;
@@ -340,11 +336,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
             if (h.x == PRIM_MISS) {
               active = false;  // a sky pixel, finished by the pass: the lane takes another
             } else if (h.x >= 0) {
-              V3 color;
-              if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
-                writeAccum(p, s, color);
-                active = false;
-              }
+              pendTri = h.x;  // shaded below with the other lanes' ray results (no walk)
+              pendT = __int_as_float(h.y);
             }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
           }
         }
@@ -364,7 +357,11 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
     if (!active) continue;
     float t;
     int tri;
-    if (PT_REGEN_YIELD > 0 && W4 && p.scene.fast) {
+    if (pendTri >= 0) {  // a camera-ray pass result: no walk
+      tri = pendTri;
+      t = pendT;
+      pendTri = -1;
+    } else if (PT_REGEN_YIELD > 0 && W4 && p.scene.fast) {
       if (!walking) {
         walk4Begin(p.scene, w, st, C);
         walking = true;
