@@ -192,8 +192,12 @@ __device__ __forceinline__ bool continueFromHit(const RenderParams& p, PathState
 // when the path has ended (its final color in `color`). A camera ray's hit and a
 // bounce ray's hit go through ONE finishHit and ONE continueFromHit (the same
 // operations on the same values as separate paths would make): the lanes of a wave
-// holding either kind shade together, and the kernel keeps one copy of the
-// shading code.
+// holding either kind shade together, and each call site of advance holds one copy
+// of the shading code (the MIS wide kernel 14.3k -> 11.0k instructions; c2 and c5
+// frame times unchanged, tools/tune.py). Shading the camera-ray pass's hits in the
+// main loop instead of the refill loop (no second call site) made the kernel smaller
+// still (7.5k) but slower -- c2 0.233 -> 0.266 ms, c5 5.55 -> 5.64 -- the lanes
+// holding them sat out a walk step before their first bounce.
 template <int INTEG>
 __device__ __forceinline__ bool advance(const RenderParams& p, PathState& s, int tri, float t, V3& color) {
   const SceneView& S = p.scene;
@@ -291,8 +295,6 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
   bool active = false;
   bool walking = false;  // PT_REGEN_YIELD: the lane's ray has a walk in progress (w, st)
-  int pendTri = -1;      // >= 0: the camera ray's result from the camera-ray pass, not yet shaded
-  float pendT = 0.0f;
   Walk4 w;
   PathState s;
   s.px = s.py = s.fr = 0;
@@ -336,8 +338,11 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
             if (h.x == PRIM_MISS) {
               active = false;  // a sky pixel, finished by the pass: the lane takes another
             } else if (h.x >= 0) {
-              pendTri = h.x;  // shaded below with the other lanes' ray results (no walk)
-              pendT = __int_as_float(h.y);
+              V3 color;
+              if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
+                writeAccum(p, s, color);
+                active = false;
+              }
             }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
           }
         }
@@ -357,11 +362,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
     if (!active) continue;
     float t;
     int tri;
-    if (pendTri >= 0) {  // a camera-ray pass result: no walk
-      tri = pendTri;
-      t = pendT;
-      pendTri = -1;
-    } else if (PT_REGEN_YIELD > 0 && W4 && p.scene.fast) {
+    if (PT_REGEN_YIELD > 0 && W4 && p.scene.fast) {
       if (!walking) {
         walk4Begin(p.scene, w, st, C);
         walking = true;
