@@ -44,7 +44,7 @@ def main():
             r.render_frames(eye, rot, 0, 100)  # policy probe (tree, split, order) + warmup
             r.synchronize()
             r.reset_stats()
-            K = 200
+            K = int(os.environ.get("PT_SHARD_FRAMES", "200"))  # 20: the driver's bench line, from an idle GPU
             t0 = time.perf_counter()
             r.render_frames(eye, rot, 100, K)
             t_sub = time.perf_counter()
