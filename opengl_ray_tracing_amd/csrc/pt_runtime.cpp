@@ -32,8 +32,8 @@ static constexpr int EV_RING = 64;
 // Frames in flight: the default megakernel's (or regen kernel's) launch g (its pipeline
 // sequence number) runs on slot stream g % depth (8 by default) with its own work queues,
 // overflow stack, tile order and camera-ray results, and writes its sample colours to colour
-// buffer g % (2 * depth + 1). While other launches are in flight its persistent grid is 1.5 /
-// depth of residency (renderOne), so the frames in flight share the GPU by space: their waves
+// buffer g % (2 * depth + 1). While k other launches are in flight its persistent grid is 1.5 /
+// (k + 1) of residency (renderOne), so the frames in flight share the GPU by space: their waves
 // are resident together, and a frame whose last long paths keep a few waves busy leaves the
 // rest of the machine to the others. Its running-mean update (mixKernel) runs on the caller's
 // stream, in frame order, once the launch's kernel has ended: the accumulation is updated in
@@ -1629,14 +1629,20 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // While other frames are in flight, each frame's grid is 150 % of its equal share: a frame
   // finishing early leaves waves of the others ready to take its place (measured against 100 /
   // 200 / 300 % with the bench line as the driver runs it, 20 frames from an idle GPU: c2 0.285 /
-  // 0.262 / 0.266 / 0.289 ms per frame at 100 / 150 / 200 / 300, c4 0.413 / 0.360 / 0.367 / 0.385)
+  // 0.262 / 0.266 / 0.289 ms per frame at 100 / 150 / 200 / 300, c4 0.413 / 0.360 / 0.367 / 0.385).
+  // The share follows the launches actually in flight, 150 % / (1 + the others still running):
+  // a launch issued into a filling pipeline (the first batches after an idle GPU) takes the
+  // machine the earlier ones leave as they drain, and a full pipeline gets 150 % / D each.
+  // 20 frames from an idle GPU, one rank's share of an N-way split (profiles/r4/shard_time_h20.jsonl,
+  // 2 runs each): c2 N = 4 0.129-0.130 -> 0.072 ms per frame, N = 8 0.061 -> 0.046-0.048, c4 N = 4
+  // 0.137 -> 0.109-0.113; N = 1, 2 and 200-frame runs within run-to-run spread.
   constexpr int GRID_PCT = 150;
   if (piped && D > 1) {
-    bool others = false;  // another frame still in flight: the caller streams frames
-    for (int k = 0; k < D && !others; k++)
-      others = k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
+    int others = 0;  // other launches still in flight: the caller streams frames
+    for (int k = 0; k < D; k++)
+      others += k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
     (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
-    if (others) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * D)));
+    if (others > 0) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * (others + 1))));
   }
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)fullGrid * bs, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
