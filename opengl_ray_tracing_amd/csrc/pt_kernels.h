@@ -66,6 +66,12 @@ constexpr int LDS_NODES = PT_LDS_NODES;
 #ifndef PT_WAVE_TRACE
 #define PT_WAVE_TRACE 0  // diagnostics build: record each megakernel wave's lifetime (tools/wave_trace.py)
 #endif
+#ifndef PT_PHASE_STATS
+// diagnostics build (with PT_WAVE_TRACE): the regen kernel's per-wave time and lanes per phase
+// (refill, walk, reference check, shading; node and leaf iterations) -- tools/wave_trace.py --phases
+#define PT_PHASE_STATS 0
+#endif
+constexpr int WAVE_TRACE_WORDS = PT_PHASE_STATS ? 16 : 6;  // u64 per wave in RenderParams::waveTrace
  // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
 #ifndef PT_NUM_QUEUES
 #define PT_NUM_QUEUES 32
@@ -215,7 +221,7 @@ struct RenderParams {
   int orderCap;         // entries per band in tileOrder
   int* tileCost;        // per tile: summed cost of its items this frame (shader cycles), null = not recorded
   int* tileCostMax;     // per tile: its longest item this frame
-  unsigned long long* waveTrace;  // PT_WAVE_TRACE builds only: 6 u64 per wave (pt_runtime.cpp, tools/wave_trace.py)
+  unsigned long long* waveTrace;  // PT_WAVE_TRACE builds only: WAVE_TRACE_WORDS u64 per wave (pt_runtime.cpp, tools/wave_trace.py)
 };
 
 struct TraceParams {

@@ -305,9 +305,35 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   const unsigned long long wStart = wall_clock64();
   unsigned long long wTiles = 0, wLastClaim = wStart, wIters = 0, wThin = 0, wLonePix = 0;
 #endif
+#if PT_PHASE_STATS
+  // diagnostics build: per wave, in LDS (first active lane adds): [0] refill cycles, [1] walk
+  // cycles, [2] reference-check cycles, [3] shading cycles, [4] main-loop iterations, [5] lanes
+  // walking, [6] lanes shading, [7]/[8] node iterations / lanes, [9]/[10] pair tests / lanes,
+  // [11] refill iterations, [12] lanes whose walk ran out of the yield, [13] walk calls that end
+  // every walk, [14] retraced lanes, [15] wave lifetime (clock64 cycles)
+  __shared__ unsigned long long s_ph[BS / 64][16];
+  unsigned long long* ph = s_ph[threadIdx.x >> 6];
+  if (lane < 16) ph[lane] = 0;
+  const long long phStart = clock64();
+#define PH_ADD(k, x)                                                         \
+  do {                                                                       \
+    const unsigned long long v_ = (unsigned long long)(x); /* every lane */ \
+    const unsigned long long m_ = __ballot(1);                               \
+    if (__lane_id() == __ffsll((unsigned long long)m_) - 1) ph[k] += v_;     \
+  } while (0)
+#else
+  unsigned long long* ph = nullptr;
+#define PH_ADD(k, x) \
+  do {               \
+  } while (0)
+#endif
   while (true) {
+#if PT_PHASE_STATS
+    const long long phA = clock64();
+#endif
     // regenerate: idle lanes take the next pixels of the wave's tile
     while (true) {
+      PH_ADD(11, 1);
       const unsigned long long idle = __ballot(!active);
       if (idle == 0) break;
       if (cursor >= 64) {
@@ -349,6 +375,9 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
       }
       cursor = min(64, cursor + __popcll(idle));
     }
+#if PT_PHASE_STATS
+    PH_ADD(0, clock64() - phA);
+#endif
     const unsigned long long act = __ballot(active);
     if (act == 0) break;
 #if PT_WAVE_TRACE
@@ -362,21 +391,44 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
     if (!active) continue;
     float t;
     int tri;
+#if PT_PHASE_STATS
+    long long phT = 0;
+#endif
     if (PT_REGEN_YIELD > 0 && W4 && p.scene.fast) {
       if (!walking) {
         walk4Begin(p.scene, w, st, C);
         walking = true;
       }
+#if PT_PHASE_STATS
+      PH_ADD(4, 1);
+      PH_ADD(5, __popcll(act));
+      phT = clock64();
+#endif
       walk4Run<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0), FULL>(p.scene, s.o, s.d, s.kind == K_SHADOW, w,
-                                                                           st, top, PT_REGEN_YIELD);
+                                                                           st, top, PT_REGEN_YIELD, ph);
+#if PT_PHASE_STATS
+      PH_ADD(1, clock64() - phT);
+      if (__ballot(!walk4Done(w)) == 0) PH_ADD(13, 1);
+      PH_ADD(12, __popcll(__ballot(!walk4Done(w))));
+#endif
       if (!walk4Done(w)) continue;  // stopped for the lanes that are done: resumes next iteration
       walking = false;
+#if PT_PHASE_STATS
+      phT = clock64();
+#endif
       t = w.tbest;
       tri = w.best >= 0 ? p.scene.fastTri[w.best] : -1;
-      if (w.tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t))) {
+      const bool retrace = w.tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t));
+      PH_ADD(14, __popcll(__ballot(retrace)));
+      if (retrace) {
         C.rays--;  // the same ray, counted once
         tri = traceRay<false, CULL, false>(p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW);
       }
+#if PT_PHASE_STATS
+      PH_ADD(2, clock64() - phT);
+      PH_ADD(6, __popcll(__ballot(1)));
+      phT = clock64();
+#endif
     } else if (W4 && p.scene.fast) {
       bool tie = false;
       const int pos = traceRay4<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0)>(p.scene, s.o, s.d, t, st, C,
@@ -395,8 +447,15 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
       writeAccum(p, s, color);
       active = false;
     }
+#if PT_PHASE_STATS
+    PH_ADD(3, clock64() - phT);
+#endif
   }
-#if PT_WAVE_TRACE
+#undef PH_ADD
+#if PT_PHASE_STATS
+  if (lane == 0) ph[15] = clock64() - phStart;
+  if (p.waveTrace && lane < 16) p.waveTrace[16 * ((size_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6)) + lane] = ph[lane];
+#elif PT_WAVE_TRACE
   if (p.waveTrace && lane == 0) {
     unsigned long long* r = p.waveTrace + 6 * ((size_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6));
     r[0] = wStart; r[1] = wall_clock64(); r[2] = wTiles | wLonePix << 32; r[3] = wLastClaim;
@@ -429,7 +488,8 @@ hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenSha
   RegenShape r;
   r.wide = wide && cull;
   const size_t treeBytes = (size_t)f4nDev * W4_F4 * sizeof(float4);
-  const size_t staticBytes = (size_t)REGEN_LDS_STACK * FULL_BS * sizeof(int) + 2 * sizeof(float4);
+  const size_t staticBytes = (size_t)REGEN_LDS_STACK * FULL_BS * sizeof(int) + 2 * sizeof(float4) +
+                             (PT_PHASE_STATS ? (size_t)FULL_BS / 64 * 16 * sizeof(unsigned long long) : 0);
   r.fullTree = PT_LDS_TREE && r.wide && integrator != 2 && wideRegenWaves(integrator) == 3 && f4nDev > 0 &&
                treeBytes + staticBytes <= LDS_BYTES;
   r.block = r.fullTree ? FULL_BS : BLOCK;

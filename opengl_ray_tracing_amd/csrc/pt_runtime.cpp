@@ -1798,7 +1798,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // diagnostics build: each wave's {start, end, tiles | longest tile's pixel << 32,
   // longest tile's duration, its most node-loop / leaf-loop iterations of a lane} (100 MHz wall
   // clock), appended per frame to $PT_WAVE_TRACE_FILE (tools/wave_trace.py)
-  const size_t nTrace = (size_t)grid * (bs / 64) * 6;
+  const size_t nTrace = (size_t)grid * (bs / 64) * WAVE_TRACE_WORDS;
   unsigned long long* dTrace = nullptr;
   {
     CK(hipMalloc(&dTrace, nTrace * sizeof(unsigned long long)));

@@ -523,7 +523,7 @@ __device__ __forceinline__ void walk4Begin(const SceneView& S, Walk4& w, StackTy
 // ALL: every node is in LDS at `top`, swizzled (loadNode4Lds); else the first S.f4nTop are, in order
 template <bool CULL, class StackType, bool LDSTOP, bool ALL = false>
 __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool anyRT, Walk4& w, StackType& st,
-                                         const float4* top, int yield) {
+                                         const float4* top, int yield, unsigned long long* ph = nullptr) {
   const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   const FusedRay fr = fusedRay(o, inv);
   const f32x2 ix = {fr.inv.x, fr.inv.x}, iy = {fr.inv.y, fr.inv.y}, iz = {fr.inv.z, fr.inv.z};
@@ -533,6 +533,10 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
     if (__ballot(!done) == 0 || __popcll(__ballot(done)) >= yield) break;  // wave-uniform
     if (done) continue;
     while (w.ref >= 0) {
+      if (PT_PHASE_STATS && ph) {  // diagnostics build: node-loop iterations (wave, lanes)
+        const unsigned long long m = __ballot(1);
+        if (__lane_id() == __ffsll((unsigned long long)m) - 1) ph[7] += 1, ph[8] += __popcll(m);
+      }
       float4 lx, ly, lz, hx, hy, hz, rf;
       if (ALL) {
         loadNode4Lds(top, w.ref, lx, ly, lz, hx, hy, hz, rf);
@@ -594,6 +598,10 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
     const int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
     w.leaf = REF_NONE;
     for (int k = 0; k < cnt; k += 2) {
+      if (PT_PHASE_STATS && ph) {  // diagnostics build: pair tests (wave, lanes)
+        const unsigned long long m = __ballot(1);
+        if (__lane_id() == __ffsll((unsigned long long)m) - 1) ph[9] += 1, ph[10] += __popcll(m);
+      }
       const int i = start + k;
       const bool second = k + 1 < cnt;
       float t0, t1;

@@ -5,6 +5,8 @@
     PT_WAVE_TRACE_FILE=gpurun_out/w.bin python tools/tune.py --child wtrace --config c4 --frames 3 --warmup 0
     python tools/wave_trace.py gpurun_out/w.bin
     python tools/wave_trace.py --regen gpurun_out/w.bin <waves per frame>   # the regen kernel's records
+    python tools/tune.py --build phases:PT_WAVE_TRACE=1,PT_PHASE_STATS=1      # the regen kernel's phases:
+    python tools/wave_trace.py --phases gpurun_out/p.bin
 
 Per frame: how long the frame lasted (first wave start to last wave end), how
 much of it the average wave was alive, the frame's tail (time from the median
@@ -43,7 +45,30 @@ def regen(path, per=None):
                         for k in last))
 
 
+PHASES = ["refill", "walk", "reference check", "shading"]
+
+
+def phases(path):
+    """PT_PHASE_STATS records (pt_regen.hip): 16 u64 per wave, summed over every wave of every frame."""
+    raw = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.float64)
+    raw = raw[raw[:, 15] > 0]
+    t = raw.sum(axis=0)
+    life = t[15]
+    print(f"{len(raw)} wave records, mean lifetime {life / len(raw) / 2.4e3:.1f} us at 2.4 GHz")
+    for k, name in enumerate(PHASES):
+        print(f"  {name:16s} {t[k] / life:6.3f} of wave time")
+    print(f"  (unaccounted      {1 - t[:4].sum() / life:6.3f})")
+    it = max(t[4], 1)
+    print(f"main-loop iterations with a walk {t[4]:.3g}: lanes walking {t[5] / it:5.1f}, lanes shading {t[6] / it:5.1f}"
+          f" (walks cut by the yield {t[12] / it:5.1f} lanes; iterations ending every walk {t[13] / it:.3f})")
+    print(f"node iterations {t[7]:.3g} ({t[7] / it:.1f} per walk call), lanes {t[8] / max(t[7], 1):5.1f} of 64")
+    print(f"pair tests      {t[9]:.3g} ({t[9] / it:.1f} per walk call), lanes {t[10] / max(t[9], 1):5.1f} of 64")
+    print(f"refill iterations {t[11]:.3g}; retraced lanes {t[14]:.3g}")
+
+
 def main():
+    if sys.argv[1] == "--phases":
+        return phases(sys.argv[2])
     if sys.argv[1] == "--regen":
         return regen(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else None)
     raw = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 6)
