@@ -1363,8 +1363,14 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
   // consumer blocks own segment blockIdx % WF_NSEG: grids are multiples of WF_NSEG
   auto segGrid = [](long g) { return (int)std::max<long>(WF_NSEG, (g + WF_NSEG - 1) / WF_NSEG * WF_NSEG); };
   const int gridC = segGrid((long)ctx->numCU * std::max(nbC, 1)), gridS = segGrid((long)ctx->numCU * std::max(nbS, 1));
+  // with the 4-wide runtime tree: one trace launch per bounce for both kinds of ray (wfTrace4Kernel)
+  const bool w4 = ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE);
+  int bs4 = 0, nb4 = 0;
+  if (w4) CK(wfTrace4Shape(cull, &bs4, &nb4));
+  const int grid4 = segGrid((long)ctx->numCU * std::max(nb4, 1));
   int ovfDepth = 0;
-  rc = ensureOverflow(ctx, (size_t)std::max(gridC, gridS) * BLOCK, &ovfDepth, WF_LDS_STACK);
+  rc = ensureOverflow(ctx, std::max((size_t)std::max(gridC, gridS) * BLOCK, (size_t)grid4 * bs4), &ovfDepth,
+                      WF_LDS_STACK);
   if (rc) return rc;
   WFParams p;
   std::memset(&p, 0, sizeof(p));
@@ -1395,6 +1401,7 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
   CK(wfLaunchGen(p, ctx->stream));
   for (int s = 0; s <= maxBounce; s++) {
     WFTraceParams t;
+    std::memset(&t, 0, sizeof(t));
     t.scene = p.scene;
     t.ovf = ovfDepth ? ctx->d_ovf : nullptr;
     t.ovfDepth = ovfDepth;
@@ -1406,6 +1413,18 @@ static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16],
     t.rayD = ctx->wf.rayD;
     t.hit = ctx->wf.hit;
     t.occ = ctx->wf.occ;
+    if (w4) {
+      t.scene.fast = 1;
+      t.scene.f4nTop = std::min(ctx->f4nDev, wfTrace4Top());
+      if (mis && s > 0) {
+        t.queueS = ctx->wfq.shd[s & 1];
+        t.countS = ctx->wfq.cnt + wfCnt(s, WF_CNT_SHD);
+        t.rayDS = ctx->wf.shD;
+      }
+      CK(wfLaunchTrace4(t, cull, grid4, ctx->stream));
+      CK(wfLaunchShade(p, c.integrator, s, gridShade, ctx->stream));
+      continue;
+    }
     CK(wfLaunchTrace(t, false, cull, gridC, ctx->stream));
     if (mis && s > 0) {
       t.queue = ctx->wfq.shd[s & 1];

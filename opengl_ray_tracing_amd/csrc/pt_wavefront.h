@@ -84,11 +84,20 @@ struct WFTraceParams {
   int* ovf;
   int ovfDepth;
   unsigned long long* rays;  // RAY_SHARDS padded ray counters
+  // wfTrace4Kernel: the env shadow rays (MIS), traced by the same launch after the closest-hit
+  // rays (null queue = none); directions rayDS, results occ
+  const int* queueS;
+  const int* countS;
+  const float4* rayDS;
 };
 
 hipError_t wfLaunchGen(const WFParams& p, hipStream_t s);
 hipError_t wfLaunchTrace(const WFTraceParams& p, bool anyhit, bool cull, int grid, hipStream_t s);
 hipError_t wfTraceBlocksPerCU(bool anyhit, bool cull, int* nb);
 hipError_t wfLaunchShade(const WFParams& p, int integrator, int stage, int grid, hipStream_t s);
+// the 4-wide runtime tree's trace kernel (p.scene.fast, p.scene.f4nTop <= wfTrace4Top())
+hipError_t wfLaunchTrace4(const WFTraceParams& p, bool cull, int grid, hipStream_t s);
+hipError_t wfTrace4Shape(bool cull, int* blockSize, int* blocksPerCU);
+int wfTrace4Top();
 
 }  // namespace pt

@@ -214,6 +214,76 @@ __global__ __launch_bounds__(BLOCK) void wfTraceKernel(WFTraceParams p) {
   addRays(p.rays, nrays);
 }
 
+// The same as a walk of the 4-wide runtime tree (pt_trace.h walk4Run), results made the
+// reference's by refReachable / a retrace through the uploaded tree as in every other frame
+// kernel. One launch traces a bounce's closest-hit rays and then its env shadow rays. A lane
+// whose walk is done writes its result and loads its next ray as soon as the wave has
+// PT_WF_YIELD such lanes, so the walks run with nearly full waves (the regen kernel's lanes
+// wait for their paths' shading instead: 16 of 64 lanes per node iteration on c5). No path
+// state is live here; the kernel is compiled for PT_WF_WAVES waves per SIMD; blocks of
+// WF4_BS threads share one LDS copy of the tree's top WF4_TOP nodes.
+#ifndef PT_WF_YIELD
+#define PT_WF_YIELD 16
+#endif
+#ifndef PT_WF_WAVES
+#define PT_WF_WAVES 4  // the walk needs ~112 VGPRs: 5 waves spill 25, 6 waves 61, 8 waves 103
+#endif
+constexpr int WF4_BS = PT_WF_WAVES >= 8 ? 1024 : PT_WF_WAVES == 5 ? 256 : 512;
+constexpr int WF4_TOP = 128;
+template <bool CULL>
+__global__ __launch_bounds__(WF4_BS, PT_WF_WAVES) void wfTrace4Kernel(WFTraceParams p) {
+  __shared__ int s_stack[WF_LDS_STACK * WF4_BS];
+  __shared__ float4 s_top[WF4_TOP * W4_F4];
+  StackT<WF_LDS_STACK, WF4_BS> st;
+  st.lds = s_stack + threadIdx.x;
+  const size_t gtid = (size_t)blockIdx.x * WF4_BS + threadIdx.x;
+  st.gbl = p.ovf ? p.ovf + gtid * p.ovfDepth : nullptr;
+  st.reset();
+  const SceneView& S = p.scene;
+  for (int i = threadIdx.x; i < S.f4nTop * W4_F4; i += WF4_BS) s_top[i] = S.fbvh4[i];
+  __syncthreads();
+  const int seg = blockIdx.x & (WF_NSEG - 1);
+  const int nC = p.count[seg * CTL_LINE_INTS];
+  const int nS = p.queueS ? p.countS[seg * CTL_LINE_INTS] : 0;
+  const int* qC = p.queue + (size_t)seg * p.segCap;
+  const int* qS = p.queueS ? p.queueS + (size_t)seg * p.segCap : nullptr;
+  const int stride = (gridDim.x / WF_NSEG) * WF4_BS;
+  int next = (blockIdx.x / WF_NSEG) * WF4_BS + threadIdx.x;
+  Counters C = {0, 0, 0, 0, 0};
+  int pid = -1;
+  bool shadow = false;
+  V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+  Walk4 w;
+  w.ref = w.leaf = REF_NONE;
+  while (true) {
+    while (pid < 0 && next < nC + nS) {
+      const bool sh = next >= nC;
+      const int c = sh ? qS[next - nC] : qC[next];
+      next += stride;
+      if (c < 0) continue;
+      o = xyz(p.rayO[c]);
+      d = xyz(sh ? p.rayDS[c] : p.rayD[c]);
+      shadow = sh;
+      pid = c;
+      walk4Begin(S, w, st, C);
+    }
+    if (__ballot(pid >= 0) == 0) break;
+    if (pid < 0) continue;
+    walk4Run<CULL, StackT<WF_LDS_STACK, WF4_BS>, true>(S, o, d, shadow, w, st, s_top, PT_WF_YIELD);
+    if (!walk4Done(w)) continue;
+    float t = w.tbest;
+    int tri = w.best >= 0 ? S.fastTri[w.best] : -1;
+    if ((w.tie && !shadow) || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
+      C.rays--;  // the same ray, counted once
+      tri = traceRay<false, CULL, false>(S, o, d, t, st, C, shadow);
+    }
+    if (shadow) p.occ[pid] = tri >= 0 ? 1 : 0;
+    else p.hit[pid] = make_int2(tri, __float_as_int(t));
+    pid = -1;
+  }
+  addRays(p.rays, C.rays);
+}
+
 // -------------------------------------------------------------- shade
 // Sample the next bounce from `hit` for the uniform-hemisphere integrators
 // (O:335-345, D:448-456): stores the pending f_r and cosine, the new ray.
@@ -428,6 +498,18 @@ hipError_t wfTraceBlocksPerCU(bool anyhit, bool cull, int* nb) {
                          : (cull ? (const void*)wfTraceKernel<false, true> : (const void*)wfTraceKernel<false, false>);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, f, BLOCK, 0);
 }
+hipError_t wfLaunchTrace4(const WFTraceParams& p, bool cull, int grid, hipStream_t s) {
+  if (p.scene.f4nTop > WF4_TOP || !p.scene.fast) return hipErrorInvalidValue;
+  if (cull) hipLaunchKernelGGL((wfTrace4Kernel<true>), dim3(grid), dim3(WF4_BS), 0, s, p);
+  else hipLaunchKernelGGL((wfTrace4Kernel<false>), dim3(grid), dim3(WF4_BS), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t wfTrace4Shape(bool cull, int* blockSize, int* blocksPerCU) {
+  *blockSize = WF4_BS;
+  const void* f = cull ? (const void*)wfTrace4Kernel<true> : (const void*)wfTrace4Kernel<false>;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, f, WF4_BS, 0);
+}
+int wfTrace4Top() { return WF4_TOP; }
 hipError_t wfLaunchShade(const WFParams& p, int integrator, int stage, int grid, hipStream_t s) {
   switch (integrator) {
     case 0: hipLaunchKernelGGL(wfShadeKernel<0>, dim3(grid), dim3(BLOCK), 0, s, p, stage); break;
