@@ -60,6 +60,12 @@ constexpr int REGEN_LDS_STACK = PT_REGEN_LDS_STACK;
 #endif
 constexpr int regenTop4W(int waves) { return waves == 3 ? PT_REGEN_TOP4_3 : PT_REGEN_TOP4; }
 
+// The camera-ray pass's results of a claimed tile loaded at once (lane k: slot k) and read by
+// the refilling lanes from their neighbours (0: each refilling lane loads its own)
+#ifndef PT_TILE_PRIM
+#define PT_TILE_PRIM 1
+#endif
+
 enum : int { K_NONE = 0, K_PRIMARY = 1, K_BOUNCE = 2, K_SHADOW = 3 };
 
 struct PathState {
@@ -293,6 +299,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   int tile = -1;      // current 8x8 wave tile (wave-uniform)
   int tileFr = 0;     // its frame in the launch's batch (wave-uniform)
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
+  int2 tileH = make_int2(PRIM_MISS, 0);  // p.primHit: lane k holds the camera-ray result of slot k of the tile
   bool active = false;
   bool walking = false;  // PT_REGEN_YIELD: the lane's ray has a walk in progress (w, st)
   Walk4 w;
@@ -345,32 +352,49 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
         wTiles++;
         wLastClaim = wall_clock64();
 #endif
+        if (PT_TILE_PRIM && p.primHit) {
+          // the whole tile's camera-ray results in one coalesced load, lane k holding slot k's: a
+          // refill then reads its slots' results from a neighbour lane instead of memory, and a
+          // tile of sky pixels (finished by the pass) is skipped without starting a path
+          const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
+          const int g = j * p.world + p.rank;
+          const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
+          const int px = gx * p.shardSize + (sI % sub) * 8 + (lane & 7);
+          const int py = gy * p.shardSize + (sI / sub) * 8 + (lane >> 3);
+          tileH = px < p.width && py < p.height ? p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px]
+                                                : make_int2(PRIM_MISS, 0);
+          if (__ballot(tileH.x != PRIM_MISS) == 0) {
+            cursor = 64;
+            continue;
+          }
+        }
       }
       const int slot = cursor + __popcll(idle & below);
+      int2 h = make_int2(0, 0);
+      if (PT_TILE_PRIM && p.primHit) h = make_int2(__shfl(tileH.x, slot & 63, 64), __shfl(tileH.y, slot & 63, 64));
       if (!active && slot < 64) {
         const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
         const int g = j * p.world + p.rank;
         const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
         const int px = gx * p.shardSize + (sI % sub) * 8 + (slot & 7);
         const int py = gy * p.shardSize + (sI / sub) * 8 + (slot >> 3);
-        if (px < p.width && py < p.height) {
+        if (!PT_TILE_PRIM && p.primHit && px < p.width && py < p.height)
+          h = p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px];
+        if (px < p.width && py < p.height && !(p.primHit && h.x == PRIM_MISS)) {
           s.px = px;
           s.py = py;
           s.fr = tileFr;
           startPath(p, s);
           active = true;
-          if (p.primHit) {  // the camera ray's result from the camera-ray pass (primaryKernel)
-            const int2 h = p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px];
-            if (h.x == PRIM_MISS) {
-              active = false;  // a sky pixel, finished by the pass: the lane takes another
-            } else if (h.x >= 0) {
-              V3 color;
-              if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
-                writeAccum(p, s, color);
-                active = false;
-              }
-            }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
-          }
+          // the camera ray's result from the camera-ray pass (primaryKernel; a sky pixel, finished
+          // by the pass, is never started: the lane takes another slot)
+          if (p.primHit && h.x >= 0) {
+            V3 color;
+            if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
+              writeAccum(p, s, color);
+              active = false;
+            }
+          }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
         }
       }
       cursor = min(64, cursor + __popcll(idle));
