@@ -584,7 +584,8 @@ __global__ void encodeKernel(const BuildNode* nodes, int M, int leafSize, const 
 }
 
 // pair records in the built order (pt_runtime.cpp buildPairs): position i holds
-// triangles order[i] (x) and order[i + 1] (y; zeros past the last)
+// triangles order[i] (x) and order[i + 1] (y; zeros past the last), and their uploaded
+// indices (the record's last two floats, as int bits; -1 past the last)
 __global__ void pairsKernel(const float4* geo, const int* order, int n, float4* pairs) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -601,7 +602,7 @@ __global__ void pairsKernel(const float4* geo, const int* order, int n, float4* 
   r[3] = make_float4(a2.x, b2.x, a2.y, b2.y);
   r[4] = make_float4(a2.z, b2.z, a3.x, b3.x);
   r[5] = make_float4(a3.y, b3.y, a3.z, b3.z);
-  r[6] = make_float4(a0.w, b0.w, 0.0f, 0.0f);
+  r[6] = make_float4(a0.w, b0.w, __int_as_float(order[i]), __int_as_float(hasB ? order[i + 1] : -1));
 }
 
 // ------------------------------------------------------------ 4-wide collapse

@@ -42,8 +42,7 @@ struct Tracer {
   __device__ __forceinline__ int trace(V3 o, V3 d, float& t) {
     if (PT_WIDE4 && !COUNT && S.fast) {  // the 4-wide runtime tree (PT_WIDE4), checked as the binary one
       bool tie = false;
-      const int pos = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, false, top, &tie);
-      int tri = pos >= 0 ? S.fastTri[pos] : -1;
+      int tri = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, false, top, &tie);
       if (tie || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
         C.rays--;
         tri = traceRay<false, CULL, false, Stack>(S, o, d, t, st, C);
@@ -74,9 +73,9 @@ struct Tracer {
     float t;
     if (PT_WIDE4 && !COUNT && S.fast) {
       bool tie = false;
-      const int pos = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, true, top, &tie);
-      if (pos < 0) return false;
-      if (refReachable(S, S.fastTri[pos], o, d, t)) return true;
+      const int tri = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, true, top, &tie);
+      if (tri < 0) return false;
+      if (refReachable(S, tri, o, d, t)) return true;
       C.rays--;
       return traceRay<true, CULL, false, Stack>(S, o, d, t, st, C) >= 0;
     }
@@ -97,8 +96,7 @@ struct Tracer {
   __device__ __forceinline__ int traceK(V3 o, V3 d, bool anyhit, float& t) {
     if (PT_WIDE4 && !COUNT && S.fast) {
       bool tie = false;
-      const int pos = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, anyhit, top, &tie);
-      int tri = pos >= 0 ? S.fastTri[pos] : -1;
+      int tri = traceRay4<CULL, Stack, (PT_WIDE4 == 2)>(S, o, d, t, st, C, anyhit, top, &tie);
       if ((tie && !anyhit) || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
         C.rays--;  // the same ray, counted once
         tri = traceRay<false, CULL, false, Stack>(S, o, d, t, st, C, anyhit);

@@ -61,7 +61,9 @@ constexpr int REGEN_LDS_STACK = PT_REGEN_LDS_STACK;
 constexpr int regenTop4W(int waves) { return waves == 3 ? PT_REGEN_TOP4_3 : PT_REGEN_TOP4; }
 
 // The camera-ray pass's results of a claimed tile loaded at once (lane k: slot k) and read by
-// the refilling lanes from their neighbours (0: each refilling lane loads its own)
+// the refilling lanes from their neighbours (0: each refilling lane loads its own). For the
+// uniform integrators only: c2 0.2226 -> 0.2173 ms per frame; the MIS kernel (4 waves, at its
+// register limit) spills more with the tile's results live, c5 5.69 -> 5.95 ms.
 #ifndef PT_TILE_PRIM
 #define PT_TILE_PRIM 1
 #endif
@@ -264,6 +266,7 @@ template <int INTEG, bool CULL, int WAVES = 0, bool W4 = false, int BS = BLOCK, 
 __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U)) void regenKernel(
     RenderParams p) {
   static_assert(!FULL || W4, "the LDS tree is the 4-wide one");
+  constexpr bool TILE_PRIM = PT_TILE_PRIM && INTEG != 2;
   __shared__ int s_stack[REGEN_LDS_STACK * BS];
   StackT<REGEN_LDS_STACK, BS> st;
   st.lds = s_stack + threadIdx.x;
@@ -352,7 +355,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
         wTiles++;
         wLastClaim = wall_clock64();
 #endif
-        if (PT_TILE_PRIM && p.primHit) {
+        if (TILE_PRIM && p.primHit) {
           // the whole tile's camera-ray results in one coalesced load, lane k holding slot k's: a
           // refill then reads its slots' results from a neighbour lane instead of memory, and a
           // tile of sky pixels (finished by the pass) is skipped without starting a path
@@ -371,14 +374,14 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
       }
       const int slot = cursor + __popcll(idle & below);
       int2 h = make_int2(0, 0);
-      if (PT_TILE_PRIM && p.primHit) h = make_int2(__shfl(tileH.x, slot & 63, 64), __shfl(tileH.y, slot & 63, 64));
+      if (TILE_PRIM && p.primHit) h = make_int2(__shfl(tileH.x, slot & 63, 64), __shfl(tileH.y, slot & 63, 64));
       if (!active && slot < 64) {
         const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
         const int g = j * p.world + p.rank;
         const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
         const int px = gx * p.shardSize + (sI % sub) * 8 + (slot & 7);
         const int py = gy * p.shardSize + (sI / sub) * 8 + (slot >> 3);
-        if (!PT_TILE_PRIM && p.primHit && px < p.width && py < p.height)
+        if (!TILE_PRIM && p.primHit && px < p.width && py < p.height)
           h = p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px];
         if (px < p.width && py < p.height && !(p.primHit && h.x == PRIM_MISS)) {
           s.px = px;
@@ -441,7 +444,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
       phT = clock64();
 #endif
       t = w.tbest;
-      tri = w.best >= 0 ? p.scene.fastTri[w.best] : -1;
+      tri = w.best;
       const bool retrace = w.tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t));
       PH_ADD(14, __popcll(__ballot(retrace)));
       if (retrace) {
@@ -455,9 +458,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
 #endif
     } else if (W4 && p.scene.fast) {
       bool tie = false;
-      const int pos = traceRay4<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0)>(p.scene, s.o, s.d, t, st, C,
-                                                                                   s.kind == K_SHADOW, top, &tie);
-      tri = pos >= 0 ? p.scene.fastTri[pos] : -1;
+      tri = traceRay4<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0)>(p.scene, s.o, s.d, t, st, C,
+                                                                         s.kind == K_SHADOW, top, &tie);
       if (tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t))) {
         C.rays--;  // the same ray, counted once
         tri = traceRay<false, CULL, false>(p.scene, s.o, s.d, t, st, C, s.kind == K_SHADOW);

@@ -703,7 +703,9 @@ static std::vector<float> refNodes(const std::vector<BuildNode>& bn, int leafSiz
 }
 
 // pair records: position i holds triangles order[i] (x) and order[i + 1] (y,
-// zeros past the last), PAIR_F4 float4 each (pt_trace.h pairTest)
+// zeros past the last), PAIR_F4 float4 each (pt_trace.h pairTest), and the two triangles'
+// uploaded indices as int bits in the last two floats (-1 past the last): a walk of the
+// runtime's tree reads its winner's index with the winner's record (pairTestIds)
 static void buildPairs(const std::vector<float4>& geo, const int* order, int nTri, std::vector<float4>& pairs) {
   pairs.assign((size_t)nTri * PAIR_F4, make_float4(0, 0, 0, 0));
   const float4 zero[4] = {make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0),
@@ -718,7 +720,11 @@ static void buildPairs(const std::vector<float4>& geo, const int* order, int nTr
     r[3] = make_float4(A[2].x, B[2].x, A[2].y, B[2].y);  // p3.x, p3.y
     r[4] = make_float4(A[2].z, B[2].z, A[3].x, B[3].x);  // p3.z, Ng.x
     r[5] = make_float4(A[3].y, B[3].y, A[3].z, B[3].z);  // Ng.y, Ng.z
-    r[6] = make_float4(A[0].w, B[0].w, 0.0f, 0.0f);      // w = dot(Ng, p1)
+    const int ia = order ? order[i] : i, ib = i + 1 < nTri ? (order ? order[i + 1] : i + 1) : -1;
+    float fa, fb;
+    std::memcpy(&fa, &ia, sizeof(fa));
+    std::memcpy(&fb, &ib, sizeof(fb));
+    r[6] = make_float4(A[0].w, B[0].w, fa, fb);          // w = dot(Ng, p1); the uploaded indices
   }
 }
 

@@ -186,8 +186,12 @@ __device__ __forceinline__ bool triTest(float4 A, float4 B, float4 C, float4 Nn,
 // packed adds and multiplies (v_pk_add_f32 / v_pk_mul_f32) round exactly like
 // the scalar ones and each pair costs about half the VALU of two triTests.
 // g0/g1: accepted apart from the caller's closest-hit bound.
-__device__ __forceinline__ void pairTest(const float4* r, V3 o, V3 d, float& t0, float& t1, bool& g0, bool& g1) {
+// ids (pairTestIds): the two triangles' uploaded indices stored in the record (buildPairs)
+template <bool IDS = false>
+__device__ __forceinline__ void pairTestT(const float4* r, V3 o, V3 d, float& t0, float& t1, bool& g0, bool& g1,
+                                          int* ids = nullptr) {
   const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6];
+  if (IDS) ids[0] = __float_as_int(q6.z), ids[1] = __float_as_int(q6.w);
   const f32x2 p1x = {q0.x, q0.y}, p1y = {q0.z, q0.w}, p1z = {q1.x, q1.y};
   const f32x2 p2x = {q1.z, q1.w}, p2y = {q2.x, q2.y}, p2z = {q2.z, q2.w};
   const f32x2 p3x = {q3.x, q3.y}, p3y = {q3.z, q3.w}, p3z = {q4.x, q4.y};
@@ -215,6 +219,16 @@ __device__ __forceinline__ void pairTest(const float4* r, V3 o, V3 d, float& t0,
        ((s1.x > 0 && s2.x > 0 && s3.x > 0) || (s1.x < 0 && s2.x < 0 && s3.x < 0));
   g1 = !(fabsf(dn.y) < 0.00001f) && !(tt.y < 0.0005f) &&
        ((s1.y > 0 && s2.y > 0 && s3.y > 0) || (s1.y < 0 && s2.y < 0 && s3.y < 0));
+}
+__device__ __forceinline__ void pairTest(const float4* r, V3 o, V3 d, float& t0, float& t1, bool& g0, bool& g1) {
+  pairTestT<false>(r, o, d, t0, t1, g0, g1);
+}
+__device__ __forceinline__ void pairTestIds(const float4* r, V3 o, V3 d, float& t0, float& t1, bool& g0, bool& g1,
+                                            int& id0, int& id1) {
+  int ids[2];
+  pairTestT<true>(r, o, d, t0, t1, g0, g1, ids);
+  id0 = ids[0];
+  id1 = ids[1];
 }
 
 __device__ __forceinline__ bool triHit(const float4* g, V3 o, V3 d, float tmax, float& t) {
@@ -361,7 +375,9 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
 // memory-latency-bound walks of large scenes (the regen kernel on scenes past
 // PT_WIDE_SCENE_MB). Results are checked exactly like the binary runtime
 // tree's (the order of visits only matters for exact-t ties, which are
-// flagged: refReachable, the retrace in the reference order).
+// flagged: refReachable, the retrace in the reference order). The walks return the
+// winner's uploaded triangle index, read from its pair record (pairTestIds), so the
+// reference check starts without a lookup of S.fastTri.
 constexpr float PT_INF_KEY = __builtin_huge_valf();  // sort key of a missed child (every entry t is finite)
 __device__ __forceinline__ void cswap(float& ka, int& ra, float& kb, int& rb) {
   const bool s = kb < ka;
@@ -473,17 +489,18 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
       const bool second = k + 1 < cnt;
       float t0, t1;
       bool g0, g1;
-      pairTest(S.fpairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1);
+      int id0, id1;
+      pairTestIds(S.fpairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1, id0, id1);
       if (g0 && t0 == tbest) *tie = true;
       if (g0 && t0 < tbest) {
         tbest = t0;
-        best = i;
+        best = id0;
         if (anyRT) { tOut = tbest; return best; }
       }
       if (g1 && second && t1 == tbest) *tie = true;
       if (g1 && second && t1 < tbest) {
         tbest = t1;
-        best = i + 1;
+        best = id1;
         if (anyRT) { tOut = tbest; return best; }
       }
     }
@@ -504,7 +521,7 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
 // lane computes), so results are identical.
 struct Walk4 {
   float tbest;
-  int best;
+  int best;  // the closest hit's uploaded triangle index (-1: none)
   int ref;   // next item in visiting order (REF_NONE: none)
   int leaf;  // parked leaf (REF_NONE: none)
   bool tie;
@@ -606,17 +623,18 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
       const bool second = k + 1 < cnt;
       float t0, t1;
       bool g0, g1;
-      pairTest(S.fpairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1);
+      int id0, id1;
+      pairTestIds(S.fpairs + PAIR_F4 * (size_t)i, o, d, t0, t1, g0, g1, id0, id1);
       if (g0 && t0 == w.tbest) w.tie = true;
       if (g0 && t0 < w.tbest) {
         w.tbest = t0;
-        w.best = i;
+        w.best = id0;
         if (anyRT) { w.ref = REF_NONE; break; }  // any hit: the walk ends here (traceRay4's return)
       }
       if (g1 && second && t1 == w.tbest) w.tie = true;
       if (g1 && second && t1 < w.tbest) {
         w.tbest = t1;
-        w.best = i + 1;
+        w.best = id1;
         if (anyRT) { w.ref = REF_NONE; break; }
       }
     }

@@ -272,7 +272,7 @@ __global__ __launch_bounds__(WF4_BS, PT_WF_WAVES) void wfTrace4Kernel(WFTracePar
     walk4Run<CULL, StackT<WF_LDS_STACK, WF4_BS>, true>(S, o, d, shadow, w, st, s_top, PT_WF_YIELD);
     if (!walk4Done(w)) continue;
     float t = w.tbest;
-    int tri = w.best >= 0 ? S.fastTri[w.best] : -1;
+    int tri = w.best;
     if ((w.tie && !shadow) || (tri >= 0 && !refReachable(S, tri, o, d, t))) {
       C.rays--;  // the same ray, counted once
       tri = traceRay<false, CULL, false>(S, o, d, t, st, C, shadow);
