@@ -277,11 +277,11 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   constexpr int TOP4 = regenTop4W(WAVES);
   constexpr int TOPF4 = FULL ? 1 : (W4 && TOP4 * W4_F4 > LDS_NODES * 4) ? TOP4 * W4_F4 : LDS_NODES * 4;
   __shared__ float4 s_nodes[TOPF4];
-  extern __shared__ float4 s_tree[];  // FULL: f4nTop * W4_F4 float4 (launch's dynamic LDS)
+  extern __shared__ float4 s_tree[];  // FULL: f4nTop * W4_LDS_F4 float4 (launch's dynamic LDS)
   if (FULL) {
     const float4* src = p.scene.fbvh4;
-    const int n = p.scene.f4nTop * W4_F4;
-    for (int i = threadIdx.x; i < n; i += BS) s_tree[swz4(i >> 3, i & 7)] = src[i];
+    const int n = p.scene.f4nTop * W4_LDS_F4;
+    for (int i = threadIdx.x; i < n; i += BS) s_tree[i] = src[W4_F4 * (i / W4_LDS_F4) + i % W4_LDS_F4];
   } else {
     const bool w4 = W4 && p.scene.fast;
     const float4* src = w4 ? p.scene.fbvh4 : p.scene.bvh;
@@ -513,7 +513,7 @@ static const void* regenFnI(int integrator, bool cull, bool wide, bool full) {
 hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenShape* out) {
   RegenShape r;
   r.wide = wide && cull;
-  const size_t treeBytes = (size_t)f4nDev * W4_F4 * sizeof(float4);
+  const size_t treeBytes = (size_t)f4nDev * W4_LDS_F4 * sizeof(float4);
   const size_t staticBytes = (size_t)REGEN_LDS_STACK * FULL_BS * sizeof(int) + 2 * sizeof(float4) +
                              (PT_PHASE_STATS ? (size_t)FULL_BS / 64 * 16 * sizeof(unsigned long long) : 0);
   r.fullTree = PT_LDS_TREE && r.wide && integrator != 2 && wideRegenWaves(integrator) == 3 && f4nDev > 0 &&
@@ -552,7 +552,7 @@ static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, b
 }
 
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, const RegenShape& r) {
-  if (r.fullTree && p.scene.f4nTop * W4_F4 * sizeof(float4) > r.dynLds) return hipErrorInvalidValue;
+  if (r.fullTree && p.scene.f4nTop * W4_LDS_F4 * sizeof(float4) > r.dynLds) return hipErrorInvalidValue;
   switch (integrator) {
     case 0: return launchRegenI<0>(p, grid, s, cull, r);
     case 1: return launchRegenI<1>(p, grid, s, cull, r);
