@@ -491,16 +491,17 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   addRays(p.rayShards, C.rays);
 }
 
-// The FULL variant: the uniform integrators' wide kernel (3 waves per SIMD) as one block of 12
-// waves per CU, the whole tree beside its 16-entry LDS stacks (PT_LDS_TREE = 0: never)
+// The FULL variant: the uniform integrators' wide kernel (PT_WIDE_REGEN_WAVES_U = 3 waves per
+// SIMD) as one block of all the CU's waves, the whole tree beside their 16-entry LDS stacks
+// (PT_LDS_TREE = 0: never)
 #ifndef PT_LDS_TREE
 #define PT_LDS_TREE 1
 #endif
-constexpr int FULL_BS = 768;
+constexpr int FULL_BS = 256 * PT_WIDE_REGEN_WAVES_U;  // one block per CU: all its waves share the tree
 constexpr size_t LDS_BYTES = 160 * 1024;
 template <int I>
 static const void* regenFn(bool cull, bool wide, bool full) {
-  if constexpr (wideRegenWaves(I) == 3)  // the 3-wave (uniform integrators') variant only
+  if constexpr (I != 2)  // the uniform integrators' variant only
     if (full) return (const void*)regenKernel<I, true, wideRegenWaves(I), true, FULL_BS, true>;
   if (wide) return (const void*)regenKernel<I, true, wideRegenWaves(I), true>;
   return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
@@ -516,7 +517,7 @@ hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenSha
   const size_t treeBytes = (size_t)f4nDev * W4_LDS_F4 * sizeof(float4);
   const size_t staticBytes = (size_t)REGEN_LDS_STACK * FULL_BS * sizeof(int) + 2 * sizeof(float4) +
                              (PT_PHASE_STATS ? (size_t)FULL_BS / 64 * 16 * sizeof(unsigned long long) : 0);
-  r.fullTree = PT_LDS_TREE && r.wide && integrator != 2 && wideRegenWaves(integrator) == 3 && f4nDev > 0 &&
+  r.fullTree = PT_LDS_TREE && r.wide && integrator != 2 && f4nDev > 0 &&
                treeBytes + staticBytes <= LDS_BYTES;
   r.block = r.fullTree ? FULL_BS : BLOCK;
   r.dynLds = r.fullTree ? treeBytes : 0;
@@ -536,7 +537,7 @@ hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenSha
 
 template <int I>
 static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, const RegenShape& r) {
-  if constexpr (wideRegenWaves(I) == 3) {
+  if constexpr (I != 2) {
     if (r.fullTree) {
       hipLaunchKernelGGL((regenKernel<I, true, wideRegenWaves(I), true, FULL_BS, true>), dim3(grid), dim3(FULL_BS),
                          r.dynLds, s, p);

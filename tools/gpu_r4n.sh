@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4 session N: texture-path busy of the c2 frame kernels (serial frames), the regen
+# kernel's phases with the current code (c2, c5).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+bash tools/gpu_ta_pass.sh c2; rc=$?; echo "ta=$rc"; [ $rc -eq 0 ] || exit $rc
+for c in c2 c5; do
+  rm -f "gpurun_out/phases_$c.bin"
+  PT_WAVE_TRACE_FILE="gpurun_out/phases_$c.bin" timeout -k 10 300 python -u tools/tune.py --child phases --config "$c" --frames 2 --warmup 0 > "gpurun_out/phases_$c.log" 2>&1; rc=$?
+  echo "phases_$c=$rc"; tail -1 "gpurun_out/phases_$c.log"; [ $rc -eq 0 ] || exit $rc
+  python tools/wave_trace.py --phases "gpurun_out/phases_$c.bin" | tee "gpurun_out/phases_$c.txt"
+done
