@@ -494,7 +494,10 @@ __device__ __forceinline__ void finishPixel(const RenderParams& p, const FrameRe
   if (INTEG == 0) Li = pathLambert(tr, p.env, first, p.maxBounce, seed, C, COUNT);
   else if (INTEG == 1) Li = pathDisneyUniform(tr, p.env, first, p.maxBounce, seed, C, COUNT);
   else Li = pathMIS(tr, p.env, first, p.maxBounce, seed, px, py, sampleIndex, C, COUNT);
-  accumulate(p, f, px, py, first.m.emissive + Li, C, COUNT);
+  // MIS (8-16 bounces): the camera hit's emission reloaded once the path has ended rather than
+  // held across every bounce (the megakernel at its 168-VGPR limit: 37 -> 28 VGPRs spilled)
+  const V3 Le0 = INTEG == 2 ? emissiveOf(p.scene, tri) : first.m.emissive;
+  accumulate(p, f, px, py, Le0 + Li, C, COUNT);
 }
 
 // ------------------------------------------------ BASIC (BasicRayTracingWithC++)

@@ -852,7 +852,19 @@ __device__ __forceinline__ void addRays(unsigned long long* shards, uint32_t r) 
 struct Hit {
   V3 P, N, viewDir;
   Material m;
+  int matId;  // m's index in S.mats
 };
+// the emission of material matId (loadMaterial's emissive), for a path that keeps the camera
+// hit's material index instead of its emission across its bounces
+__device__ __forceinline__ V3 emissiveMat(const SceneView& S, int matId) {
+  const float4* m = S.mats + MAT_F4 * (size_t)matId;
+  const float4 a = m[0], b = m[1];
+  return v3(a.z, a.w, b.x);
+}
+// the emission of triangle tri's material (finishHit's h.m.emissive)
+__device__ __forceinline__ V3 emissiveOf(const SceneView& S, int tri) {
+  return emissiveMat(S, __float_as_int(S.hitRec[HIT_F4 * (size_t)tri + 2].y));
+}
 __device__ __forceinline__ void finishHit(const SceneView& S, int tri, V3 o, V3 d, float t, Hit& h) {
   // the triangle's vertices and normal from its pair record (the x halves), the
   // record the leaf test of an uploaded-tree traversal has just read
@@ -873,7 +885,8 @@ __device__ __forceinline__ void finishHit(const SceneView& S, int tri, V3 o, V3 
   h.P = P;
   h.N = inside ? -Ns : Ns;
   h.viewDir = d;
-  h.m = loadMaterial(S.mats + MAT_F4 * (size_t)__float_as_int(q2.y));
+  h.matId = __float_as_int(q2.y);
+  h.m = loadMaterial(S.mats + MAT_F4 * (size_t)h.matId);
 }
 
 }  // namespace pt
