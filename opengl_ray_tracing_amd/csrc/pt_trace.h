@@ -140,6 +140,15 @@ struct FusedRay {
   V3 inv, noi;
 };
 __device__ __forceinline__ float clampInv(float v) { return copysignf(fminf(fabsf(v), 0x1p64f), v); }
+// fma(a, s.x, s.y) on both halves of a, s = {1/d, -o/d} of one axis, as two scalar FMAs: a
+// 4-wide walk holds its ray as three such pairs. Packed FMAs need both scalars broadcast into
+// register pairs of their own (six pairs, twelve VGPRs, live across the whole walk); the
+// scalar form has six VGPRs fewer and twelve more VALU instructions per visit, and measured
+// faster everywhere (c2 0.2122 -> 0.2056 ms, c4 0.2926 -> 0.2775, c5 5.59 -> 5.51; spills of
+// the MIS kernels 28 -> 13 and 88 -> 76 VGPRs). The same IEEE fma, so the same results.
+__device__ __forceinline__ f32x2 fmaBcast(f32x2 a, f32x2 s) {
+  return f32x2{__builtin_fmaf(a.x, s.x, s.y), __builtin_fmaf(a.y, s.x, s.y)};
+}
 __device__ __forceinline__ FusedRay fusedRay(V3 o, V3 inv) {
   FusedRay f;
   f.inv = v3(clampInv(inv.x), clampInv(inv.y), clampInv(inv.z));
@@ -181,44 +190,43 @@ __device__ __forceinline__ bool triTest(float4 A, float4 B, float4 C, float4 Nn,
   t = tt;
   return !(fabsf(dn) < 0.00001f) && !(tt < 0.0005f) && (tt < tmax) && (r1 || r2);
 }
-// triTest of triangles i and i+1 at once from their pair record (pt_runtime.cpp):
-// every operation of triTest on float2 pairs (x = triangle i, y = i+1), so the
-// packed adds and multiplies (v_pk_add_f32 / v_pk_mul_f32) round exactly like
-// the scalar ones and each pair costs about half the VALU of two triTests.
+// triTest of triangles i and i+1 from their pair record (pt_runtime.cpp): the two triangles'
+// data arrive in one memory round trip, component-interleaved. Every operation of triTest per
+// triangle, in scalar VALU. (Until round 4 the pair ran as packed v_pk_mul/v_pk_add math, half
+// the VALU, but with o and d broadcast into six register pairs that the compiler hoists out of
+// the walks and holds across them: scalar, the Lambert LDS-tree kernel drops 159 -> 135 VGPRs
+// and the MIS kernels' spills 13 -> 2 (megakernel) and 76 -> 14 (regen), c2 0.2029 -> 0.1931 ms,
+// c4 0.2888 -> 0.2803, c5 5.48 -> 5.34.)
 // g0/g1: accepted apart from the caller's closest-hit bound.
 // ids (pairTestIds): the two triangles' uploaded indices stored in the record (buildPairs)
+__device__ __forceinline__ void pairHalf(float p1x, float p1y, float p1z, float p2x, float p2y, float p2z, float p3x,
+                                         float p3y, float p3z, float nx, float ny, float nz, float w, V3 o, V3 d,
+                                         float& t, bool& g) {
+  const float dn = (nx * d.x + ny * d.y) + nz * d.z;        // dot(N, d)
+  const float num = w - ((o.x * nx + o.y * ny) + o.z * nz);  // A.w - dot(o, N)
+  const float tt = num / dn;
+  const float Px = o.x + d.x * tt, Py = o.y + d.y * tt, Pz = o.z + d.z * tt;
+  // dot(cross(b - a, P - a), N)
+  auto edge = [&](float ax, float ay, float az, float bx, float by, float bz) -> float {
+    const float ex = bx - ax, ey = by - ay, ez = bz - az;
+    const float vx = Px - ax, vy = Py - ay, vz = Pz - az;
+    const float cx = ey * vz - vy * ez, cy = ez * vx - vz * ex, cz = ex * vy - vx * ey;
+    return (cx * nx + cy * ny) + cz * nz;
+  };
+  const float s1 = edge(p1x, p1y, p1z, p2x, p2y, p2z);
+  const float s2 = edge(p2x, p2y, p2z, p3x, p3y, p3z);
+  const float s3 = edge(p3x, p3y, p3z, p1x, p1y, p1z);
+  t = tt;
+  g = !(fabsf(dn) < 0.00001f) && !(tt < 0.0005f) && ((s1 > 0 && s2 > 0 && s3 > 0) || (s1 < 0 && s2 < 0 && s3 < 0));
+}
 template <bool IDS = false>
 __device__ __forceinline__ void pairTestT(const float4* r, V3 o, V3 d, float& t0, float& t1, bool& g0, bool& g1,
                                           int* ids = nullptr) {
   const float4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6];
   if (IDS) ids[0] = __float_as_int(q6.z), ids[1] = __float_as_int(q6.w);
-  const f32x2 p1x = {q0.x, q0.y}, p1y = {q0.z, q0.w}, p1z = {q1.x, q1.y};
-  const f32x2 p2x = {q1.z, q1.w}, p2y = {q2.x, q2.y}, p2z = {q2.z, q2.w};
-  const f32x2 p3x = {q3.x, q3.y}, p3y = {q3.z, q3.w}, p3z = {q4.x, q4.y};
-  const f32x2 nx = {q4.z, q4.w}, ny = {q5.x, q5.y}, nz = {q5.z, q5.w};
-  const f32x2 w = {q6.x, q6.y};
-  const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-  const f32x2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
-  const f32x2 dn = (nx * dx + ny * dy) + nz * dz;           // dot(N, d)
-  const f32x2 num = w - ((ox * nx + oy * ny) + oz * nz);    // A.w - dot(o, N)
-  const f32x2 tt = {num.x / dn.x, num.y / dn.y};
-  const f32x2 Px = ox + dx * tt, Py = oy + dy * tt, Pz = oz + dz * tt;
-  // dot(cross(b - a, P - a), N)
-  auto edge = [&](f32x2 ax, f32x2 ay, f32x2 az, f32x2 bx, f32x2 by, f32x2 bz) -> f32x2 {
-    const f32x2 ex = bx - ax, ey = by - ay, ez = bz - az;
-    const f32x2 vx = Px - ax, vy = Py - ay, vz = Pz - az;
-    const f32x2 cx = ey * vz - vy * ez, cy = ez * vx - vz * ex, cz = ex * vy - vx * ey;
-    return (cx * nx + cy * ny) + cz * nz;
-  };
-  const f32x2 s1 = edge(p1x, p1y, p1z, p2x, p2y, p2z);
-  const f32x2 s2 = edge(p2x, p2y, p2z, p3x, p3y, p3z);
-  const f32x2 s3 = edge(p3x, p3y, p3z, p1x, p1y, p1z);
-  t0 = tt.x;
-  t1 = tt.y;
-  g0 = !(fabsf(dn.x) < 0.00001f) && !(tt.x < 0.0005f) &&
-       ((s1.x > 0 && s2.x > 0 && s3.x > 0) || (s1.x < 0 && s2.x < 0 && s3.x < 0));
-  g1 = !(fabsf(dn.y) < 0.00001f) && !(tt.y < 0.0005f) &&
-       ((s1.y > 0 && s2.y > 0 && s3.y > 0) || (s1.y < 0 && s2.y < 0 && s3.y < 0));
+  // (p1.x, p1.y, p1.z, p2.x, ..., Ng.z, w) of triangle i in the x halves, i + 1 in the y halves
+  pairHalf(q0.x, q0.z, q1.x, q1.z, q2.x, q2.z, q3.x, q3.z, q4.x, q4.z, q5.x, q5.z, q6.x, o, d, t0, g0);
+  pairHalf(q0.y, q0.w, q1.y, q1.w, q2.y, q2.w, q3.y, q3.w, q4.y, q4.w, q5.y, q5.w, q6.y, o, d, t1, g1);
 }
 __device__ __forceinline__ void pairTest(const float4* r, V3 o, V3 d, float& t0, float& t1, bool& g0, bool& g1) {
   pairTestT<false>(r, o, d, t0, t1, g0, g1);
@@ -411,8 +419,7 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
                                          bool anyRT, const float4* top, bool* tie) {
   const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   const FusedRay fr = fusedRay(o, inv);
-  const f32x2 ix = {fr.inv.x, fr.inv.x}, iy = {fr.inv.y, fr.inv.y}, iz = {fr.inv.z, fr.inv.z};
-  const f32x2 ox = {fr.noi.x, fr.noi.x}, oy = {fr.noi.y, fr.noi.y}, oz = {fr.noi.z, fr.noi.z};
+  const f32x2 sx = {fr.inv.x, fr.noi.x}, sy = {fr.inv.y, fr.noi.y}, sz = {fr.inv.z, fr.noi.z};
   float tbest = PT_INF;
   int best = -1;
   int ref = S.f4Root;
@@ -437,10 +444,8 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
         const f32x2 Lx = h ? f32x2{lx.z, lx.w} : f32x2{lx.x, lx.y}, Ly = h ? f32x2{ly.z, ly.w} : f32x2{ly.x, ly.y};
         const f32x2 Lz = h ? f32x2{lz.z, lz.w} : f32x2{lz.x, lz.y}, Hx = h ? f32x2{hx.z, hx.w} : f32x2{hx.x, hx.y};
         const f32x2 Hy = h ? f32x2{hy.z, hy.w} : f32x2{hy.x, hy.y}, Hz = h ? f32x2{hz.z, hz.w} : f32x2{hz.x, hz.y};
-        const f32x2 fx = __builtin_elementwise_fma(Hx, ix, ox), fy = __builtin_elementwise_fma(Hy, iy, oy),
-                    fz = __builtin_elementwise_fma(Hz, iz, oz);
-        const f32x2 nx = __builtin_elementwise_fma(Lx, ix, ox), ny = __builtin_elementwise_fma(Ly, iy, oy),
-                    nz = __builtin_elementwise_fma(Lz, iz, oz);
+        const f32x2 fx = fmaBcast(Hx, sx), fy = fmaBcast(Hy, sy), fz = fmaBcast(Hz, sz);
+        const f32x2 nx = fmaBcast(Lx, sx), ny = fmaBcast(Ly, sy), nz = fmaBcast(Lz, sz);
 #pragma unroll
         for (int e = 0; e < 2; e++) {
           const int c = 2 * h + e;
@@ -545,8 +550,7 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
                                          const float4* top, int yield, unsigned long long* ph = nullptr) {
   const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   const FusedRay fr = fusedRay(o, inv);
-  const f32x2 ix = {fr.inv.x, fr.inv.x}, iy = {fr.inv.y, fr.inv.y}, iz = {fr.inv.z, fr.inv.z};
-  const f32x2 ox = {fr.noi.x, fr.noi.x}, oy = {fr.noi.y, fr.noi.y}, oz = {fr.noi.z, fr.noi.z};
+  const f32x2 sx = {fr.inv.x, fr.noi.x}, sy = {fr.inv.y, fr.noi.y}, sz = {fr.inv.z, fr.noi.z};
   while (true) {
     const bool done = walk4Done(w);
     if (__ballot(!done) == 0 || __popcll(__ballot(done)) >= yield) break;  // wave-uniform
@@ -572,10 +576,8 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
         const f32x2 Lx = h ? f32x2{lx.z, lx.w} : f32x2{lx.x, lx.y}, Ly = h ? f32x2{ly.z, ly.w} : f32x2{ly.x, ly.y};
         const f32x2 Lz = h ? f32x2{lz.z, lz.w} : f32x2{lz.x, lz.y}, Hx = h ? f32x2{hx.z, hx.w} : f32x2{hx.x, hx.y};
         const f32x2 Hy = h ? f32x2{hy.z, hy.w} : f32x2{hy.x, hy.y}, Hz = h ? f32x2{hz.z, hz.w} : f32x2{hz.x, hz.y};
-        const f32x2 fx = __builtin_elementwise_fma(Hx, ix, ox), fy = __builtin_elementwise_fma(Hy, iy, oy),
-                    fz = __builtin_elementwise_fma(Hz, iz, oz);
-        const f32x2 nx = __builtin_elementwise_fma(Lx, ix, ox), ny = __builtin_elementwise_fma(Ly, iy, oy),
-                    nz = __builtin_elementwise_fma(Lz, iz, oz);
+        const f32x2 fx = fmaBcast(Hx, sx), fy = fmaBcast(Hy, sy), fz = fmaBcast(Hz, sz);
+        const f32x2 nx = fmaBcast(Lx, sx), ny = fmaBcast(Ly, sy), nz = fmaBcast(Lz, sz);
 #pragma unroll
         for (int e = 0; e < 2; e++) {
           const int c = 2 * h + e;
