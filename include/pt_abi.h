@@ -100,9 +100,10 @@ typedef struct pt_config {
   int device_ids[PT_MAX_DEVICES];
   int gather;
   /* ABI 6 */
-  int frame_batch;    /* pt_render_frames_async: most frames per launch (0 = automatic: 2 x tile_world
-                         frames, about two whole images' work per launch; tile_world on scenes of more
-                         than 48 MB of records with the Disney/MIS integrators) */
+  int frame_batch;    /* pt_render_frames_async: most frames per launch, at most 16 (0 = automatic:
+                         2 x tile_world frames with the Lambert integrator, 4 x tile_world with
+                         Disney/MIS, tile_world with Disney/MIS on scenes of more than 48 MB of
+                         records) */
   int hw_queues;      /* hardware queues of the process's HIP runtime (GPU_MAX_HW_QUEUES in effect when
                          HIP initialised; bounds the frames in flight); 0 = read GPU_MAX_HW_QUEUES now */
 } pt_config;

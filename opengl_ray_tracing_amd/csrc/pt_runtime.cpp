@@ -283,15 +283,20 @@ int pt_device_count(int* n) {
 
 const char* pt_last_error(pt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
-// Frames per launch of pt_render_frames_async: pt_config.frame_batch, else two whole images' work
-// per launch (2 x tile_world frames) -- one image's is enough to fill the machine, the second
-// halves the launches and running-mean updates per frame: c2 0.244 -> 0.231 ms per frame at N = 1,
-// c4 0.326 -> 0.318, c2's 1/8 share 0.0354 -> 0.0344, c4's 0.0477 -> 0.0446 (profiles/r4) -- and
-// one image's on large Disney/MIS scenes (c5 5.66 ms at 1, 5.86 at 2 frames per launch).
+// Frames per launch of pt_render_frames_async: pt_config.frame_batch, else whole images' work per
+// launch in multiples of tile_world frames, at most MAX_BATCH:
+//  * 2 x for the Lambert regen kernel -- one image's is enough to fill the machine, the second
+//    halves the launches and running-mean updates per frame: c2 0.244 -> 0.231 ms per frame at
+//    N = 1, c2's 1/8 share 0.0354 -> 0.0344 (profiles/r4); 3 and 4 measured no better;
+//  * 4 x for the megakernel (Disney/MIS on small scenes), whose longest-first launches end in their
+//    longest tiles: c4 at N = 1 0.2566 -> 0.2531 ms per frame over 200 frames and 0.3288 -> 0.2860
+//    over 20 from an idle GPU, N = 2 0.139 -> 0.131, N = 4 / 8 equal (profiles/r4/batch_c4/);
+//  * 1 x on large Disney/MIS scenes, whose frames are long already (c5 5.66 ms at 1, 5.86 at 2).
 static int batchFor(const pt_ctx* ctx, bool wideScene) {
   const pt_config& c = ctx->cfg;
   if (c.frame_batch > 0) return std::min(c.frame_batch, MAX_BATCH);
-  return std::max(1, std::min((wideScene ? 1 : 2) * std::max(1, c.tile_world), MAX_BATCH));
+  const int m = wideScene ? 1 : c.integrator == 0 ? 2 : 4;
+  return std::max(1, std::min(m * std::max(1, c.tile_world), MAX_BATCH));
 }
 
 static int createOne(pt_ctx** out, const pt_config* cfg) {

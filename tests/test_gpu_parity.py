@@ -341,7 +341,8 @@ def test_frame_batches_equal_serial_frames(request, name, tile, batch, flags):
     a, sa = run(0, True)
     b, sb = run(FLAG_SERIAL_FRAMES, False)
     assert sa.frames == sb.frames == sum(c[2] for c in calls)
-    assert sa.frame_batch == (batch or min(2 * tile[1], 16)) and sa.launches < sa.frames
+    auto = min((2 if cfg.integrator == "lambert" else 4) * tile[1], 16)  # pt_runtime.cpp batchFor
+    assert sa.frame_batch == (batch or auto) and sa.launches < sa.frames
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert sa.rays == sb.rays
