@@ -40,8 +40,12 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "gpurun_out"
-TRACE_STEPS = 30    # tools/gpu_profile.sh: --steps 30 under --kernel-trace (pipelined and serial)
-COUNTER_STEPS = 10  # --steps 10 under each --pmc pass
+# tools/gpu_profile.sh: --steps 32 under --kernel-trace (pipelined and serial), --steps 16 under each
+# --pmc pass -- multiples of every automatic frames-per-launch (1, 2, 4, 8, 16), so the last
+# steps / F dispatches are exactly the timed frames (round 4's first c4 profile at 30 / 10 with F = 4
+# averaged a 2-frame launch in and under-counted its frames by a quarter)
+TRACE_STEPS = 32
+COUNTER_STEPS = 16
 FRAME_KERNELS = {
     "primary": re.compile(r"primaryKernel"),
     "frame": re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true[^>]*>"),
