@@ -35,10 +35,11 @@ constexpr int WIDE_WAVES = 3;
 #ifndef PT_WIDE_REGEN_WAVES
 #define PT_WIDE_REGEN_WAVES 4  // MIS
 #endif
-// the uniform integrators' (Lambert, Disney) variant: 3 waves per SIMD leave its 163 VGPRs unspilled
-// (4 waves: 128 VGPRs, 59 spilled): c2 0.241 -> 0.235 ms per frame (5 waves: 0.313)
+// the uniform integrators' (Lambert, Disney) variant: 4 waves per SIMD since round 4's scalar pair
+// test (128 VGPRs, 3 spilled; 3 waves 135 unspilled): c2 0.1938 -> 0.1884 ms per frame (5 rounds,
+// profiles/r4/ab/aj_*). Before it, 3 waves (163 VGPRs) against 4 (59 spilled): 0.235 vs 0.241 ms.
 #ifndef PT_WIDE_REGEN_WAVES_U
-#define PT_WIDE_REGEN_WAVES_U 3
+#define PT_WIDE_REGEN_WAVES_U 4
 #endif
 constexpr int WIDE_REGEN_WAVES = PT_WIDE_REGEN_WAVES;
 constexpr int wideRegenWaves(int integrator) { return integrator == 2 ? PT_WIDE_REGEN_WAVES : PT_WIDE_REGEN_WAVES_U; }

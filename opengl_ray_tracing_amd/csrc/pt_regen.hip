@@ -503,7 +503,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   addRays(p.rayShards, C.rays);
 }
 
-// The FULL variant: the uniform integrators' wide kernel (PT_WIDE_REGEN_WAVES_U = 3 waves per
+// The FULL variant: the uniform integrators' wide kernel (PT_WIDE_REGEN_WAVES_U = 4 waves per
 // SIMD) as one block of all the CU's waves, the whole tree beside their 16-entry LDS stacks
 // (PT_LDS_TREE = 0: never)
 #ifndef PT_LDS_TREE
