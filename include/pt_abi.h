@@ -53,7 +53,8 @@ extern "C" {
 #define PT_FLAG_NO_CULL 0x1u      /* traverse exactly like pass1.fsh:335-382 (no closest-t culling) */
 #define PT_FLAG_CLOSEST_SHADOW 0x2u /* env shadow rays use closest-hit instead of any-hit */
 #define PT_FLAG_COUNT_FETCHES 0x4u /* count reference-algorithm fetches (implies NO_CULL, closest shadow) */
-#define PT_FLAG_WAVEFRONT 0x8u    /* staged wavefront pipeline instead of the persistent megakernel */
+#define PT_FLAG_WAVEFRONT 0x8u    /* retired (round 5): the staged wavefront pipeline measured slower than the
+                                     regen kernel on every config; pt_create rejects it (PT_E_INVALID) */
 #define PT_FLAG_REGEN 0x10u       /* path-regeneration state-machine kernel instead of the megakernel */
 #define PT_FLAG_NO_TILE_ORDER 0x20u /* megakernel: hand out tiles in fixed order, not longest-first */
 #define PT_FLAG_REFERENCE_TREE 0x40u /* megakernel: traverse only the uploaded tree (not the runtime's own) */

@@ -42,15 +42,12 @@ CXX_FLAGS = ["-O2", "-fPIC", "-pthread", "-std=c++17", "-ffp-contract=off", "-fn
 SOURCES = {
     "pt_kernels.o": ("hip", CSRC / "pt_kernels.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h", CSRC / "pt_trace.h", INCLUDE / "pt_scene.h",
                                                        INCLUDE / "pt_fmath.h"]),
-    "pt_wavefront.o": ("hip", CSRC / "pt_wavefront.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h",
-                                                           CSRC / "pt_trace.h", CSRC / "pt_wavefront.h",
-                                                           INCLUDE / "pt_fmath.h"]),
     "pt_regen.o": ("hip", CSRC / "pt_regen.hip", [CSRC / "pt_device.h", CSRC / "pt_kernels.h", CSRC / "pt_trace.h",
                                                    INCLUDE / "pt_fmath.h"]),
     "pt_envcache.o": ("hip", CSRC / "pt_envcache.hip", [CSRC / "pt_kernels.h"]),
     "pt_primary.o": ("hip", CSRC / "pt_primary.hip", [CSRC / "pt_kernels.h"]),
     "pt_build.o": ("hip", CSRC / "pt_build.hip", [CSRC / "pt_kernels.h"]),
-    "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", CSRC / "pt_wavefront.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
+    "pt_runtime.o": ("cxx", CSRC / "pt_runtime.cpp", [CSRC / "pt_kernels.h", INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h",
                                                        INCLUDE / "pt_fmath.h", CSRC / "pt_rccl.h"]),
     "pt_rccl.o": ("cxx", CSRC / "pt_rccl.cpp", [CSRC / "pt_rccl.h"]),
     "scene.o": ("cxx", CSRC / "scene.cpp", [INCLUDE / "pt_scene.h"]),
@@ -123,6 +120,20 @@ def build_variant(name: str, defines: dict, hip_flags=()) -> Path:
     return lib
 
 
+ABI_CALLER_SRC = ROOT / "tests" / "native" / "abi_caller.cpp"
+ABI_CALLER = ROOT / "tests" / "native" / "abi_caller"
+
+
+def build_abi_caller(force: bool = False) -> Path:
+    """Test infrastructure: the compiled reference-side caller of the C ABI (tests/native/abi_caller.cpp,
+    INTEGRATION.md's DisneyBRDF display() loop), g++ against include/*.h and -lpt only."""
+    deps = [ABI_CALLER_SRC, INCLUDE / "pt_abi.h", INCLUDE / "pt_scene.h", LIB]
+    if force or _stale(ABI_CALLER, deps):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", str(ABI_CALLER_SRC), f"-I{INCLUDE}", f"-L{PKG}", "-lpt",
+              "-Wl,-rpath,$ORIGIN/../../opengl_ray_tracing_amd", "-o", str(ABI_CALLER)])
+    return ABI_CALLER
+
+
 def build_oracle(force: bool = False) -> Path:
     """Test infrastructure only (see oracle/pt_oracle.h)."""
     src = [ORACLE_DIR / "pt_oracle.c", ORACLE_DIR / "pt_oracle.h", ORACLE_DIR / "Makefile", INCLUDE / "pt_fmath.h"]
@@ -134,5 +145,6 @@ def build_oracle(force: bool = False) -> Path:
 if __name__ == "__main__":
     build_native(force="--force" in sys.argv, verbose=True)
     build_oracle(force="--force" in sys.argv)
+    build_abi_caller(force="--force" in sys.argv)
     print(LIB)
     print(ORACLE_LIB)

@@ -861,8 +861,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
     RenderParams p) {
   __shared__ int s_stack[LDS_STACK * BLOCK];
   Stack st;
-  st.lds = s_stack + threadIdx.x;
-  st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * p.ovfDepth : nullptr;
+  st.init(s_stack, p.ovf, p.ovfDepth);
   st.reset();
   // the top of the tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
@@ -988,9 +987,8 @@ template <bool CULL>
 __global__ __launch_bounds__(BLOCK) void traceKernel(TraceParams p) {
   __shared__ int s_stack[LDS_STACK * BLOCK];
   Stack st;
-  st.lds = s_stack + threadIdx.x;
+  st.init(s_stack, p.ovf, p.ovfDepth);
   const size_t gtid = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-  st.gbl = p.ovf ? p.ovf + gtid * p.ovfDepth : nullptr;
   Counters C = {0, 0, 0, 0, 0};
   SceneView S = p.scene;  // no LDS copy of the top of the tree here
   S.nTop = 0;

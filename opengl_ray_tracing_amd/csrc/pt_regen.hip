@@ -114,6 +114,23 @@ __device__ __forceinline__ V3 camEmission(const RenderParams& p, const PathState
   return INTEG == 2 ? emissiveMat(p.scene, s.mat0) : s.Le0;
 }
 
+// the set bits of a wave-wide mask below the calling lane (v_mbcnt: no 64-bit lane mask held in VGPRs)
+__device__ __forceinline__ int rankBelow(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// the first pixel of 8x8 wave tile `tile` of this context's screen-tile share
+__device__ __forceinline__ int tilePx(const RenderParams& p, int tile, int sub) {
+  const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
+  const int g = j * p.world + p.rank;
+  return (g % p.shardsX) * p.shardSize + (sI % sub) * 8;
+}
+__device__ __forceinline__ int tilePy(const RenderParams& p, int tile, int sub) {
+  const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
+  const int g = j * p.world + p.rank;
+  return (g / p.shardsX) * p.shardSize + (sI / sub) * 8;
+}
+
 // main IS:846-850: seed and camera ray of pixel (px, py)
 __device__ __forceinline__ void startPath(const RenderParams& p, PathState& s) {
   const int W = p.width, H = p.height;
@@ -281,8 +298,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   constexpr bool TILE_PRIM = PT_TILE_PRIM && INTEG != 2;
   __shared__ int s_stack[REGEN_LDS_STACK * BS];
   StackT<REGEN_LDS_STACK, BS> st;
-  st.lds = s_stack + threadIdx.x;
-  st.gbl = p.ovf ? p.ovf + (size_t)(blockIdx.x * BS + threadIdx.x) * p.ovfDepth : nullptr;
+  st.init(s_stack, p.ovf, p.ovfDepth);
   st.reset();
   // the top of the tree (every ray's first node visits) -- or all of it -- staged in LDS once per block
 #if PT_LDS_NODES > 0
@@ -307,14 +323,21 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
 #endif
   Counters C = {0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
-  const unsigned long long below = (1ull << lane) - 1ull;
   const int home = blockIdx.x & (NUM_QUEUES - 1);
   const int sub = p.shardSize >> 3;
   TileCursor cur;     // wave-uniform
   int tile = -1;      // current 8x8 wave tile (wave-uniform)
   int tileFr = 0;     // its frame in the launch's batch (wave-uniform)
-  int cursor = 64;    // next unused pixel slot of the tile (wave-uniform)
-  int2 tileH = make_int2(PRIM_MISS, 0);  // p.primHit: lane k holds the camera-ray result of slot k of the tile
+  int cursor = 64;    // next unused pixel slot of the tile (wave-uniform; TILE_PRIM: index into s_slot)
+  int nValid = 0;     // TILE_PRIM: slots of the tile that need a path (wave-uniform)
+  bool drained = false;  // TILE_PRIM: the work queues had nothing left for this wave (wave-uniform)
+  // TILE_PRIM: the tile's slots that need a path, in slot order, and their camera-ray results (this
+  // wave's rows; in LDS rather than registers, which the walk needs)
+  __shared__ unsigned char s_slotAll[TILE_PRIM ? BS : 1];
+  __shared__ int2 s_hitAll[TILE_PRIM ? BS : 1];
+  const int waveBase = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));  // scalar
+  unsigned char* s_slot = s_slotAll + (TILE_PRIM ? waveBase : 0);
+  int2* s_hit = s_hitAll + (TILE_PRIM ? waveBase : 0);
   bool active = false;
   bool walking = false;  // PT_REGEN_YIELD: the lane's ray has a walk in progress (w, st)
   Walk4 w;
@@ -353,66 +376,126 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
 #if PT_PHASE_STATS
     const long long phA = clock64();
 #endif
-    // regenerate: idle lanes take the next pixels of the wave's tile
-    while (true) {
-      PH_ADD(11, 1);
-      const unsigned long long idle = __ballot(!active);
-      if (idle == 0) break;
-      if (cursor >= 64) {
-        const int item = cur.next(p.queue, p.perQueue, p.numItems, home, tileFr, p.nFrames);
-        if (item < 0) break;  // no tiles left for this wave
-        tile = item;
-        cursor = 0;
+    if constexpr (TILE_PRIM) {
+      // regenerate (uniform integrators): idle lanes take the next pixels of the wave's tile that
+      // need a path -- the claimed tile's camera-ray results are loaded at once (lane k: slot k)
+      // and its non-sky slots compacted into s_slot, so one pass hands every idle lane a pixel
+      // (sky pixels, finished by the camera-ray pass, are never handed out) -- and then the camera
+      // hits taken here are shaded together, once (shading inside the hand-out loop ran that code
+      // once per hand-out pass, for a few lanes each time)
+      while (true) {
+        bool pend = false;
+        int2 hP = make_int2(0, 0);
+        while (true) {
+          PH_ADD(11, 1);
+          const unsigned long long idle = __ballot(!active);
+          if (idle == 0) break;
+          if (cursor >= nValid) {
+            const int item = cur.next(p.queue, p.perQueue, p.numItems, home, tileFr, p.nFrames);
+            if (item < 0) {
+              drained = true;
+              break;  // no tiles left for this wave
+            }
+            tile = item;
 #if PT_WAVE_TRACE
-        wTiles++;
-        wLastClaim = wall_clock64();
+            wTiles++;
+            wLastClaim = wall_clock64();
 #endif
-        if (TILE_PRIM && p.primHit) {
-          // the whole tile's camera-ray results in one coalesced load, lane k holding slot k's: a
-          // refill then reads its slots' results from a neighbour lane instead of memory, and a
-          // tile of sky pixels (finished by the pass) is skipped without starting a path
-          const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
-          const int g = j * p.world + p.rank;
-          const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
-          const int px = gx * p.shardSize + (sI % sub) * 8 + (lane & 7);
-          const int py = gy * p.shardSize + (sI / sub) * 8 + (lane >> 3);
-          tileH = px < p.width && py < p.height ? p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px]
-                                                : make_int2(PRIM_MISS, 0);
-          if (__ballot(tileH.x != PRIM_MISS) == 0) {
-            cursor = 64;
-            continue;
+            const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
+            const int g = j * p.world + p.rank;
+            const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
+            const int px = gx * p.shardSize + (sI % sub) * 8 + (lane & 7);
+            const int py = gy * p.shardSize + (sI / sub) * 8 + (lane >> 3);
+            const bool in = px < p.width && py < p.height;
+            // without the camera-ray pass every pixel's camera ray is traced here (PRIM_RETRACE)
+            const int2 h = !in ? make_int2(PRIM_MISS, 0)
+                               : p.primHit ? p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px]
+                                           : make_int2(PRIM_RETRACE, 0);
+            const unsigned long long valid = __ballot(h.x != PRIM_MISS);
+            if (h.x != PRIM_MISS) {
+              const int k = rankBelow(valid);
+              s_slot[k] = (unsigned char)lane;
+              s_hit[k] = h;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            nValid = __popcll(valid);
+            cursor = 0;
+            continue;  // an all-sky tile (nValid 0) is skipped without starting a path
           }
+          const int r = cursor + rankBelow(idle);
+          if (!active && r < nValid) {
+            const int slot = s_slot[r];
+            const int2 h = s_hit[r];
+            s.px = tilePx(p, tile, sub) + (slot & 7);
+            s.py = tilePy(p, tile, sub) + (slot >> 3);
+            s.fr = tileFr;
+            active = true;
+            pend = true;
+            hP = h;
+          }
+          cursor = min(nValid, cursor + __popcll(idle));
         }
-      }
-      const int slot = cursor + __popcll(idle & below);
-      int2 h = make_int2(0, 0);
-      if (TILE_PRIM && p.primHit) h = make_int2(__shfl(tileH.x, slot & 63, 64), __shfl(tileH.y, slot & 63, 64));
-      if (!active && slot < 64) {
-        const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
-        const int g = j * p.world + p.rank;
-        const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
-        const int px = gx * p.shardSize + (sI % sub) * 8 + (slot & 7);
-        const int py = gy * p.shardSize + (sI / sub) * 8 + (slot >> 3);
-        if (!TILE_PRIM && p.primHit && px < p.width && py < p.height)
-          h = p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px];
-        if (px < p.width && py < p.height && !(p.primHit && h.x == PRIM_MISS)) {
-          s.px = px;
-          s.py = py;
-          s.fr = tileFr;
+        // the camera hits just taken, shaded together (a PRIM_RETRACE / PRIM_TILE camera ray is
+        // traced below like any ray)
+        bool ended = false;
+        if (pend) {
           startPath(p, s);
-          active = true;
-          // the camera ray's result from the camera-ray pass (primaryKernel; a sky pixel, finished
-          // by the pass, is never started: the lane takes another slot)
-          if (p.primHit && h.x >= 0) {
+          if (hP.x >= 0) {
             V3 color;
-            if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
+            if (!advance<INTEG>(p, s, hP.x, __int_as_float(hP.y), color)) {
               writeAccum(p, s, color);
               active = false;
+              ended = true;
             }
-          }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
+          }
         }
+        // a path that ended at its camera hit (max_bounce 0) leaves its lane idle: hand out again
+        if (drained || __ballot(ended) == 0) break;
       }
-      cursor = min(64, cursor + __popcll(idle));
+    } else {
+      // regenerate: idle lanes take the next pixels of the wave's tile
+      while (true) {
+        PH_ADD(11, 1);
+        const unsigned long long idle = __ballot(!active);
+        if (idle == 0) break;
+        if (cursor >= 64) {
+          const int item = cur.next(p.queue, p.perQueue, p.numItems, home, tileFr, p.nFrames);
+          if (item < 0) break;  // no tiles left for this wave
+          tile = item;
+          cursor = 0;
+#if PT_WAVE_TRACE
+          wTiles++;
+          wLastClaim = wall_clock64();
+#endif
+        }
+        const int slot = cursor + rankBelow(idle);
+        if (!active && slot < 64) {
+          const int px = tilePx(p, tile, sub) + (slot & 7);
+          const int py = tilePy(p, tile, sub) + (slot >> 3);
+          int2 h = make_int2(0, 0);
+          if (p.primHit && px < p.width && py < p.height)
+            h = p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px];
+          if (px < p.width && py < p.height && !(p.primHit && h.x == PRIM_MISS)) {
+            s.px = px;
+            s.py = py;
+            s.fr = tileFr;
+            startPath(p, s);
+            active = true;
+            // the camera ray's result from the camera-ray pass (primaryKernel; a sky pixel, finished
+            // by the pass, is never started: the lane takes another slot)
+            if (p.primHit && h.x >= 0) {
+              V3 color;
+              if (!advance<INTEG>(p, s, h.x, __int_as_float(h.y), color)) {
+                writeAccum(p, s, color);
+                active = false;
+              }
+            }  // PRIM_RETRACE / PRIM_TILE: traced below like any camera ray
+          }
+        }
+        cursor = min(64, cursor + __popcll(idle));
+      }
     }
 #if PT_PHASE_STATS
     PH_ADD(0, clock64() - phA);

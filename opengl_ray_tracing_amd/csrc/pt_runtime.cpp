@@ -24,7 +24,6 @@
 #include "pt_kernels.h"
 #include "pt_rccl.h"
 #include "pt_scene.h"
-#include "pt_wavefront.h"
 
 using namespace pt;
 
@@ -197,10 +196,6 @@ struct pt_ctx {
   int* d_tri = nullptr;
   size_t traceCap = 0;
   float* d_rgb = nullptr;
-  // wavefront pipeline state (allocated on first use)
-  WFState wf{};
-  WFQueues wfq{};
-  bool wfReady = false;
   // in-process multi-GPU (pt_config.n_devices > 1): this context renders as
   // screen-tile rank 0 on device_ids[0] and owns the other ranks' contexts and
   // the per-frame gather of their tiles into its accumulation
@@ -270,8 +265,6 @@ static int upload(pt_ctx* ctx, T** dst, const std::vector<T>& src) {
 
 extern "C" {
 
-static void freeWavefront(pt_ctx* ctx);
-
 int pt_device_count(int* n) {
   if (!n) return PT_E_INVALID;
   int c = 0;
@@ -308,6 +301,10 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
       cfg->tile_world < 1 || cfg->tile_rank < 0 || cfg->tile_rank >= cfg->tile_world || cfg->sample_world < 0 ||
       cfg->sample_rank < 0 || cfg->sample_rank >= (cfg->sample_world > 0 ? cfg->sample_world : 1)) {
     g_create_err = "pt_create: invalid config";
+    return PT_E_INVALID;
+  }
+  if (cfg->flags & PT_FLAG_WAVEFRONT) {  // retired in round 5; git history keeps it
+    g_create_err = "pt_create: invalid config: PT_FLAG_WAVEFRONT (the staged wavefront pipeline) was retired";
     return PT_E_INVALID;
   }
   int ndev = 0;
@@ -361,9 +358,9 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   ctx->numItems = owned * (ss / 8) * (ss / 8);
   ctx->perQueue = (ctx->numItems + NUM_QUEUES - 1) / NUM_QUEUES;
   // the default megakernel and the regen kernel pipeline their frames (not BASIC, the fetch
-  // counter, the wavefront pipeline or PT_FLAG_SERIAL_FRAMES)
+  // counter or PT_FLAG_SERIAL_FRAMES)
   ctx->pipe = cfg->integrator != PT_BASIC_CPU_COMPAT &&
-              !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_WAVEFRONT | PT_FLAG_SERIAL_FRAMES));
+              !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_SERIAL_FRAMES));
   if (ctx->pipe) {
     // a process has the hardware queues its HIP runtime was initialised with (GPU_MAX_HW_QUEUES,
     // HIP's default 4; the Python package asks for 12 when it is unset and HIP not yet initialised,
@@ -467,7 +464,6 @@ void pt_destroy(pt_ctx* ctx) {
     if (ctx->mixDone[k]) (void)hipEventDestroy(ctx->mixDone[k]);
   }
   if (ctx->binsBuilt) (void)hipEventDestroy(ctx->binsBuilt);
-  freeWavefront(ctx);
   for (hipEvent_t e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
@@ -1309,147 +1305,6 @@ static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDep
   return PT_OK;
 }
 
-// ------------------------------------------------------------ wavefront pipeline
-// counter stages of the wavefront pipeline: gen + one per bounce + the last shade's output
-static int wfStages(const pt_ctx* ctx) {
-  const int mb = ctx->cfg.max_bounce >= 0 ? ctx->cfg.max_bounce : defaultBounce(ctx->cfg.integrator);
-  return std::min(mb, 250) + 2;
-}
-
-static int ensureWavefront(pt_ctx* ctx) {
-  if (ctx->wfReady) return PT_OK;
-  const size_t n = (size_t)ctx->cfg.width * ctx->cfg.height;
-  WFState& s = ctx->wf;
-  CK(hipMalloc(&s.rayO, n * sizeof(float4)));
-  CK(hipMalloc(&s.rayD, n * sizeof(float4)));
-  CK(hipMalloc(&s.shD, n * sizeof(float4)));
-  CK(hipMalloc(&s.hit, n * sizeof(int2)));
-  CK(hipMalloc(&s.occ, n * sizeof(int)));
-  CK(hipMalloc(&s.seed, n * sizeof(uint32_t)));
-  CK(hipMalloc(&s.flags, n * sizeof(uint32_t)));
-  CK(hipMalloc(&s.hist, n * sizeof(float4)));
-  CK(hipMalloc(&s.Lo, n * sizeof(float4)));
-  CK(hipMalloc(&s.Le0, n * sizeof(float4)));
-  CK(hipMalloc(&s.pend, n * sizeof(float4)));
-  CK(hipMalloc(&s.shC, n * sizeof(float4)));
-  // segment s of a queue holds the wave tiles s, s+WF_NSEG, ... of the frame
-  const size_t tiles = (size_t)ctx->numItems;
-  ctx->wfq.segCap = (int)(((tiles + WF_NSEG - 1) / WF_NSEG) * 64);
-  const size_t qn = (size_t)WF_NSEG * ctx->wfq.segCap;
-  for (int k = 0; k < 2; k++) {
-    CK(hipMalloc(&ctx->wfq.act[k], qn * sizeof(int)));
-    CK(hipMalloc(&ctx->wfq.cls[k], qn * sizeof(int)));
-    CK(hipMalloc(&ctx->wfq.shd[k], qn * sizeof(int)));
-  }
-  CK(hipMalloc(&ctx->wfq.cnt, wfCnt(wfStages(ctx) + 1, 0) * sizeof(int)));
-  ctx->wfReady = true;
-  return PT_OK;
-}
-
-static void freeWavefront(pt_ctx* ctx) {
-  WFState& s = ctx->wf;
-  dfree(s.rayO); dfree(s.rayD); dfree(s.shD); dfree(s.hit); dfree(s.occ); dfree(s.seed);
-  dfree(s.flags); dfree(s.hist); dfree(s.Lo); dfree(s.Le0); dfree(s.pend); dfree(s.shC);
-  for (int k = 0; k < 2; k++) {
-    dfree(ctx->wfq.act[k]); dfree(ctx->wfq.cls[k]); dfree(ctx->wfq.shd[k]);
-  }
-  dfree(ctx->wfq.cnt);
-  ctx->wfReady = false;
-}
-
-// gen -> [trace closest (+ shadow) -> shade] x (maxBounce + 1), all on ctx->stream
-static int renderWavefront(pt_ctx* ctx, const float eye[3], const float cam[16], uint32_t frameCounter, bool cull,
-                           unsigned long long* stats, hipEvent_t evb, hipEvent_t eve) {
-  const pt_config& c = ctx->cfg;
-  (void)stats;
-  unsigned long long* rayShards = reinterpret_cast<unsigned long long*>(ctx->d_ctl + CTL_RAYS);
-  int rc = ensureWavefront(ctx);
-  if (rc) return rc;
-  const int maxBounce = c.max_bounce >= 0 ? c.max_bounce : defaultBounce(c.integrator);
-  if (maxBounce > 250) return fail(ctx, PT_E_INVALID, "max_bounce too large for the wavefront pipeline");
-  const bool mis = c.integrator == PT_DISNEY_MIS_SOBOL_IS;
-  int nbC = 0, nbS = 0;
-  CK(wfTraceBlocksPerCU(false, cull, &nbC));
-  CK(wfTraceBlocksPerCU(true, cull, &nbS));
-  // consumer blocks own segment blockIdx % WF_NSEG: grids are multiples of WF_NSEG
-  auto segGrid = [](long g) { return (int)std::max<long>(WF_NSEG, (g + WF_NSEG - 1) / WF_NSEG * WF_NSEG); };
-  const int gridC = segGrid((long)ctx->numCU * std::max(nbC, 1)), gridS = segGrid((long)ctx->numCU * std::max(nbS, 1));
-  // with the 4-wide runtime tree: one trace launch per bounce for both kinds of ray (wfTrace4Kernel)
-  const bool w4 = ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE);
-  int bs4 = 0, nb4 = 0;
-  if (w4) CK(wfTrace4Shape(cull, &bs4, &nb4));
-  const int grid4 = segGrid((long)ctx->numCU * std::max(nb4, 1));
-  int ovfDepth = 0;
-  rc = ensureOverflow(ctx, std::max((size_t)std::max(gridC, gridS) * BLOCK, (size_t)grid4 * bs4), &ovfDepth,
-                      WF_LDS_STACK);
-  if (rc) return rc;
-  WFParams p;
-  std::memset(&p, 0, sizeof(p));
-  p.scene = sceneView(ctx);
-  p.env.hdr = ctx->d_hdr;
-  p.env.cache = ctx->d_cache;
-  p.env.w = ctx->hdrW;
-  p.env.h = ctx->hdrH;
-  p.env.res = ctx->hdrW;
-  p.st = ctx->wf;
-  p.q = ctx->wfq;
-  p.accum = ctx->d_accum;
-  p.width = c.width;
-  p.height = c.height;
-  p.frameCounter = frameCounter;
-  p.sampleIndex = sampleIndex(c, frameCounter);
-  p.maxBounce = maxBounce;
-  std::memcpy(p.eye, eye, sizeof(p.eye));
-  std::memcpy(p.cam, cam, sizeof(p.cam));
-  p.numOwned = ctx->numItems * 64;
-  p.shardSize = ctx->shardSize;
-  p.shardsX = ctx->shardsX;
-  p.rank = c.tile_rank;
-  p.world = c.tile_world;
-  CK(hipMemsetAsync(ctx->wfq.cnt, 0, wfCnt(maxBounce + 2, 0) * sizeof(int), ctx->stream));
-  const int gridShade = segGrid(std::min<long>(((long)p.numOwned + BLOCK - 1) / BLOCK, (long)ctx->numCU * 16));
-  CK(hipEventRecord(evb, ctx->stream));
-  CK(wfLaunchGen(p, ctx->stream));
-  for (int s = 0; s <= maxBounce; s++) {
-    WFTraceParams t;
-    std::memset(&t, 0, sizeof(t));
-    t.scene = p.scene;
-    t.ovf = ovfDepth ? ctx->d_ovf : nullptr;
-    t.ovfDepth = ovfDepth;
-    t.rays = rayShards;
-    t.rayO = ctx->wf.rayO;
-    t.segCap = ctx->wfq.segCap;
-    t.queue = ctx->wfq.cls[s & 1];
-    t.count = ctx->wfq.cnt + wfCnt(s, WF_CNT_CLS);
-    t.rayD = ctx->wf.rayD;
-    t.hit = ctx->wf.hit;
-    t.occ = ctx->wf.occ;
-    if (w4) {
-      t.scene.fast = 1;
-      t.scene.f4nTop = std::min(ctx->f4nDev, wfTrace4Top());
-      if (mis && s > 0) {
-        t.queueS = ctx->wfq.shd[s & 1];
-        t.countS = ctx->wfq.cnt + wfCnt(s, WF_CNT_SHD);
-        t.rayDS = ctx->wf.shD;
-      }
-      CK(wfLaunchTrace4(t, cull, grid4, ctx->stream));
-      CK(wfLaunchShade(p, c.integrator, s, gridShade, ctx->stream));
-      continue;
-    }
-    CK(wfLaunchTrace(t, false, cull, gridC, ctx->stream));
-    if (mis && s > 0) {
-      t.queue = ctx->wfq.shd[s & 1];
-      t.count = ctx->wfq.cnt + wfCnt(s, WF_CNT_SHD);
-      t.rayD = ctx->wf.shD;
-      CK(wfLaunchTrace(t, true, cull, gridS, ctx->stream));
-    }
-    CK(wfLaunchShade(p, c.integrator, s, gridShade, ctx->stream));
-  }
-  CK(hipEventRecord(eve, ctx->stream));
-  commitLaunch(ctx);
-  return PT_OK;
-}
-
 // Two policies are chosen by measurement, since results are identical either
 // way and which is faster depends on the scene and the integrator:
 //  * the tree: the runtime's own (binned SAH; results checked against the
@@ -1597,12 +1452,6 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (!ctx->d_bvh || !eye || !cameraRotate) return fail(ctx, ctx->d_bvh ? PT_E_INVALID : PT_E_NOSCENE, "no scene");
   const bool count = (c.flags & PT_FLAG_COUNT_FETCHES) != 0;
   const bool cull = !count && !(c.flags & PT_FLAG_NO_CULL);
-  if (!count && (c.flags & PT_FLAG_WAVEFRONT)) {
-    CK(hipMemsetAsync(ctx->d_ctl + CTL_QUEUES, 0, (size_t)NUM_QUEUES * CTL_LINE_INTS * sizeof(int), ctx->stream));
-    int erc = launchEvents(ctx, &evb, &eve);
-    if (erc) return erc;
-    return renderWavefront(ctx, eye, cameraRotate, frameCounter, cull, stats, evb, eve);
-  }
   // default: the lock-step persistent megakernel (also the fetch-counting
   // variant); the path-regeneration kernel on request, and by default for the
   // Disney/MIS integrators on large scenes (pt_kernels.h PT_WIDE_SCENE_MB,

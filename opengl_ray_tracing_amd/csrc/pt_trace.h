@@ -1,6 +1,6 @@
 // pt_trace.h -- BVH traversal and triangle intersection shared by the
-// megakernel (pt_kernels.hip) and the wavefront trace kernels
-// (pt_wavefront.hip). Restates hitBVH / hitArray / hitTriangle / hitAABB of
+// megakernel (pt_kernels.hip), the path-regeneration kernel (pt_regen.hip) and the
+// camera-ray pass (pt_primary.hip). Restates hitBVH / hitArray / hitTriangle / hitAABB of
 // ImportanceSampling_LowDiscrepancySequence/shaders/pass1.fsh:251-382 over the
 // re-laid-out device scene (pt_kernels.h SceneView).
 #pragma once
@@ -18,7 +18,7 @@ struct Counters {
 // LDS stack of up to DEPTH entries per lane, entry e of thread t at
 // lds[(e % DEPTH) * STRIDE + t] (lane-interleaved: a wave's push/pop is bank
 // conflict free). Entries [0, base) live in the thread's HBM overflow region
-// gbl[] (only trees deeper than DEPTH get there): a push onto a full LDS part
+// the thread's overflow region gbl() (only trees deeper than DEPTH get there): a push onto a full LDS part
 // moves its older half to HBM, and a pop from an empty LDS part brings back up
 // to half a stack at once -- one memory round trip per DEPTH/2 pops. (Moving
 // one entry per push/pop past the LDS depth stalled every deep pop on an L2
@@ -28,14 +28,26 @@ template <int DEPTH, int STRIDE>
 struct StackT {
   static_assert((DEPTH & (DEPTH - 1)) == 0, "LDS stack depth must be a power of two");
   static constexpr int HALF = DEPTH / 2;
-  int* lds;   // &s_stack[threadIdx.x]
-  int* gbl;   // overflow region (may be null when maxStack <= DEPTH)
-  int sp;     // entries on the stack
-  int base;   // entries in gbl
+  int* lds;       // &s_stack[threadIdx.x]
+  int* ovf;       // the launch's overflow area (RenderParams::ovf, wave-uniform; may be null when
+  int ovfDepth;   // maxStack <= DEPTH), ovfDepth entries per thread: this thread's region is
+                  // computed where it is used (a per-lane pointer held across every walk cost two
+                  // VGPRs: the regen kernel's spills)
+  int sp;         // entries on the stack
+  int base;       // entries in the overflow region
+  __device__ __forceinline__ void init(int* ldsBase, int* ovfArea, int depth) {
+    lds = ldsBase + threadIdx.x;
+    ovf = ovfArea;
+    ovfDepth = depth;
+  }
+  __device__ __forceinline__ int* gbl() const {
+    return ovf + ((size_t)blockIdx.x * STRIDE + threadIdx.x) * (size_t)ovfDepth;
+  }
   __device__ __forceinline__ void reset() { sp = 0; base = 0; }
   __device__ __forceinline__ void push(int v) {
     if (sp - base == DEPTH) {
-      for (int i = 0; i < HALF; i++) gbl[base + i] = lds[((base + i) & (DEPTH - 1)) * STRIDE];
+      int* g = gbl();
+      for (int i = 0; i < HALF; i++) g[base + i] = lds[((base + i) & (DEPTH - 1)) * STRIDE];
       base += HALF;
     }
     lds[(sp & (DEPTH - 1)) * STRIDE] = v;
@@ -45,7 +57,8 @@ struct StackT {
     if (sp == base) {
       const int n = base < HALF ? base : HALF;
       base -= n;
-      for (int i = 0; i < n; i++) lds[((base + i) & (DEPTH - 1)) * STRIDE] = gbl[base + i];
+      const int* g = gbl();
+      for (int i = 0; i < n; i++) lds[((base + i) & (DEPTH - 1)) * STRIDE] = g[base + i];
     }
     sp--;
     return lds[(sp & (DEPTH - 1)) * STRIDE];
@@ -823,7 +836,7 @@ struct TileCursor {
       const int q = (home + qi) & (NUM_QUEUES - 1);
       int it = 0;
       if ((threadIdx.x & 63) == 0) it = atomicAdd(queue + q * CTL_LINE_INTS, 1);
-      it = __shfl(it, 0, 64);
+      it = __builtin_amdgcn_readfirstlane(it);  // lane 0's claim, as a scalar (the item is wave-uniform)
       const int k = nFrames == 1 ? it : it / nFrames;
       if (order) {
         if (it < order[NUM_QUEUES * orderCap + q] * nFrames) {

@@ -28,7 +28,7 @@ INTEGRATORS = {
 FLAG_NO_CULL = 0x1
 FLAG_CLOSEST_SHADOW = 0x2
 FLAG_COUNT_FETCHES = 0x4
-FLAG_WAVEFRONT = 0x8
+FLAG_WAVEFRONT = 0x8  # retired in round 5: pt_create rejects it (include/pt_abi.h)
 FLAG_REGEN = 0x10
 FLAG_NO_TILE_ORDER = 0x20
 FLAG_REFERENCE_TREE = 0x40

@@ -16,6 +16,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libpt.so on the GPU)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    config.addinivalue_line("markers", "perf: wall-clock assertion, run only with PT_PERF_TESTS=1")
 
 
 @pytest.fixture(scope="session", autouse=True)
@@ -26,4 +27,6 @@ def _native_built():
         _build.build_native()
     if not _build.ORACLE_LIB.exists():
         _build.build_oracle()
+    if not _build.ABI_CALLER.exists():
+        _build.build_abi_caller()
     yield

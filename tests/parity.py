@@ -1,11 +1,15 @@
 """Parity metrics shared by the GPU tests (test infrastructure).
 
-Tolerances (DESIGN.md "Parity"): float32 path tracing where +,-,*,/,sqrt round
-identically on both sides and the transcendentals (ocml vs glibc) may differ
-by ~1 ulp. A 1-ulp difference can flip a discrete branch (edge hit, lobe
-choice, Russian roulette) and change a 1-spp pixel completely, so the bar is:
+What is asserted: the GPU and the CPU restatement evaluate the same
+float32 operations in the same order (+,-,*,/,sqrt IEEE on both sides, the
+transcendentals from the one shared include/pt_fmath.h), so images are equal BIT FOR
+BIT -- `exact == 1.0` is asserted by default, which is what README/DESIGN claim.
+The stated tolerance bar of SURVEY.md 8(c) / BASELINE.md is asserted as well and
+reported in every failure message, so a regression shows how far it is off:
   * per-pixel relative L2 <= 1e-3 on >= 99.9 % of compared pixels,
-  * image-mean relative L2 <= 1e-4 over the compared pixels.
+  * image-mean relative L2 <= 1e-4 over the compared pixels,
+  * linear PSNR >= 60 dB (peak = the oracle image's maximum; inf when exact).
+A case that is not bit-exact by construction passes exact=False and keeps the bar.
 """
 from __future__ import annotations
 
@@ -14,6 +18,7 @@ import numpy as np
 PIX_TOL = 1e-3
 PIX_FRAC = 0.999
 MEAN_TOL = 1e-4
+PSNR_MIN_DB = 60.0
 
 
 def rel_l2(g: np.ndarray, o: np.ndarray) -> np.ndarray:
@@ -43,11 +48,15 @@ def summary(g: np.ndarray, o: np.ndarray) -> dict:
     }
 
 
-def assert_parity(g, o, what=""):
+def assert_parity(g, o, what="", exact=True):
     s = summary(g, o)
+    bar = f"(bar: within {PIX_TOL} on >= {PIX_FRAC}, mean <= {MEAN_TOL}, PSNR >= {PSNR_MIN_DB} dB)"
     assert s["finite"], f"{what}: non-finite GPU values {s}"
-    assert s["within"] >= PIX_FRAC, f"{what}: per-pixel parity {s}"
-    assert s["mean_rel"] <= MEAN_TOL, f"{what}: image-mean parity {s}"
+    assert s["within"] >= PIX_FRAC, f"{what}: per-pixel parity {s} {bar}"
+    assert s["mean_rel"] <= MEAN_TOL, f"{what}: image-mean parity {s} {bar}"
+    assert s["psnr"] >= PSNR_MIN_DB, f"{what}: linear PSNR {s} {bar}"
+    if exact:
+        assert s["exact"] == 1.0, f"{what}: not bit-exact against the oracle {s} {bar}"
     return s
 
 

@@ -75,3 +75,15 @@ def test_product_does_not_link_oracle():
     out = subprocess.run(["readelf", "-d", str(_build.LIB)], capture_output=True, text=True, check=True).stdout
     assert "oracle" not in out
     assert "orc_" not in " ".join(exported_symbols(_build.LIB))
+
+
+def test_compiled_cpp_caller_links_against_the_headers_only():
+    """tests/native/abi_caller.cpp -- INTEGRATION.md's DisneyBRDF display() loop and BVH's debug
+    ray as a C++ program built with g++ against include/pt_abi.h + pt_scene.h and -lpt -- links
+    and loads libpt.so without a GPU (--version calls pt_abi_version only)."""
+    exe = _build.build_abi_caller()
+    out = subprocess.run([str(exe), "--version"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert int(out.stdout) == _native.load().pt_abi_version()
+    need = subprocess.run(["readelf", "-d", str(exe)], capture_output=True, text=True, check=True).stdout
+    assert "libpt.so" in need and "oracle" not in need
