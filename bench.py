@@ -48,10 +48,11 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
-# hardware queues for the renderer's frames in flight (one stream each, pt_runtime.cpp depthStep),
-# set before torch or the renderer first initialises HIP (HIP's default is 4)
-if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 12:
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+# hardware queues for the renderer's frames in flight (one stream each, pt_runtime.cpp depthStep):
+# the package's one policy (opengl_ray_tracing_amd/__init__.py, also what the tests run under) --
+# 12 when GPU_MAX_HW_QUEUES is unset, an explicit value respected (at most 32) -- applied at import,
+# before torch or the renderer first initialises HIP; the line reports the value in effect
+import opengl_ray_tracing_amd  # noqa: E402,F401
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # VALU issue: 1024 SIMD-32s (256 CUs x 4) each issue one wave64 VALU instruction per 2 cycles
@@ -162,15 +163,16 @@ def main():
         from opengl_ray_tracing_amd.distributed import SampleReduce
         combine = SampleReduce(r, rank, n, f"cuda:{local}")
 
-    batch = r.stats().frame_batch  # frames per launch (the renderer's; 1 at N = 1)
+    batch = r.stats().frame_batch  # frames per launch = frames per gather (the renderer's: 2 x N for Lambert)
 
-    def frames(first, n, cam=None):
-        """frames first .. first+n-1: batches of `batch` frames (one launch each, every frame its own
-        1 spp and running-mean update), each followed by the gather to rank 0 when N > 1"""
+    def frames(first, n, cam=None, per=None):
+        """frames first .. first+n-1: batches of `per` (default `batch`) frames (one launch each, every
+        frame its own 1 spp and running-mean update), each followed by the gather to rank 0 when N > 1"""
         e, c = cam if cam is not None else (eye, rot)
+        per = per or batch
         k = 0
         while k < n:
-            m = min(batch, n - k)
+            m = min(per, n - k)
             r.render_frames(e, c, first + k, m)
             if gather is not None:
                 gather()
@@ -196,6 +198,16 @@ def main():
     sync_all()
     t1 = time.perf_counter()
     st = r.stats()
+    # N > 1: the same steps with one gather per frame (one frame per launch), the cadence at which
+    # the reference presents (IS main.cpp:706), timed the same way -- reported next to the batched
+    # figure, whose image reaches rank 0 once per batch of `batch` frames
+    per_frame_ms = None
+    if gather is not None and batch > 1:
+        sync_all()
+        t4 = time.perf_counter()
+        frames(PROBE_FRAMES + args.warmup + args.steps, args.steps, per=1)
+        sync_all()
+        per_frame_ms = 1e3 * (time.perf_counter() - t4) / args.steps
     # interactive cost after a camera move (the reference's mouse() rotates the camera and zeroes
     # frameCounter, OpenglRayTracing/main.cpp:611-634): frames 0..PROBE_FRAMES-1 of a restarted
     # running mean from a camera rotated by one degree, timed like the steps -- the camera-ray
@@ -252,6 +264,10 @@ def main():
             rs = torch.tensor([reset_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(rs, op=dist.ReduceOp.MAX)
             reset_ms = float(rs[0].item())
+        if per_frame_ms is not None:
+            pf = torch.tensor([per_frame_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(pf, op=dist.ReduceOp.MAX)
+            per_frame_ms = float(pf[0].item())
         rays_total = float(sm[1].item())
         kernel_ms_avg = float(mx[2].item()) / max(st.launches, 1)
     else:
@@ -298,7 +314,8 @@ def main():
                        "traversal_tree": "runtime (checked against uploaded)" if st.runtime_tree else "uploaded",
                        "frame_kernel": "path regeneration" if st.regen else "lock-step megakernel",
                        "waves_per_simd": st.waves_per_simd, "frames_in_flight": st.frames_in_flight,
-                       "frames_per_launch": batch,
+                       "hw_queues": opengl_ray_tracing_amd.HW_QUEUES,
+                       "frames_per_launch": batch, "frames_per_gather": batch if n > 1 else None,
                        "parallelism": (f"screen-tile x{n}" + ((f" + RCCL gather of the displayed frame (RGB8) per "
                                                                f"batch of {batch} frames" if args.gather == "display"
                                                                else f" + RCCL gather of the running means (f32 "
@@ -311,6 +328,10 @@ def main():
         }
         if combined_finite is not None:
             line["config"]["combined_image_finite"] = combined_finite
+        if per_frame_ms is not None:  # the same frames with a gather after every frame
+            line["gather_every_frame"] = {"ms_per_step": round(per_frame_ms, 4),
+                                          "value": round(rays_total / (per_frame_ms * 1e-3 * args.steps) / 1e6, 2),
+                                          "unit": "Mrays/s", "frames_per_gather": 1}
         print(json.dumps(line), flush=True)
     r.close()
     if n > 1:

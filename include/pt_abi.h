@@ -26,12 +26,14 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 6  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
+#define PT_ABI_VERSION 7  /* 2: in-process multi-GPU fields at the end of pt_config / pt_frame_stats;
                              3: scene-upload fields at the end of pt_frame_stats, pt_build_bvh_device;
                              4: BASIC shapes as doubles, its double image, the replayed random stream;
                              5: the displayed frame of a screen-tile split (pt_display_*);
                              6: batches of frames (pt_render_frames_async, pt_config.frame_batch,
-                                pt_frame_stats.frames), pt_config.hw_queues */
+                                pt_frame_stats.frames), pt_config.hw_queues;
+                             7: pt_unpack_ranks (every other rank's f32 gather in one launch);
+                                PT_FLAG_WAVEFRONT retired */
 
 /* error codes */
 #define PT_OK 0
@@ -255,6 +257,9 @@ int pt_tonemap(pt_ctx* ctx, float limit, float gamma, float* rgb_out);
 int pt_owned_pixel_count(pt_ctx* ctx, int rank, int world, int64_t* count);
 int pt_pack_owned(pt_ctx* ctx, void* dpacked);
 int pt_unpack_rank(pt_ctx* ctx, int rank, int world, const void* dpacked);
+/* pt_unpack_rank of ranks 1..world-1 in one launch (dpacked[k] = rank k's packed buffer, [0] unused,
+ * a NULL entry is skipped; world <= 16): rank 0's reassembly after a gather of the running means. */
+int pt_unpack_ranks(pt_ctx* ctx, int world, const void* const* dpacked);
 
 /* The displayed frame (pass3.fsh:14-24 drawn into the 8-bit GLUT_RGBA window,
  * ImportanceSampling_LowDiscrepancySequence/main.cpp:706,747): tonemap (and gamma > 0)

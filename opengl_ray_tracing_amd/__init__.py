@@ -26,7 +26,7 @@ def _hw_queues(want: int = 12) -> int:
     cur = os.environ.get("GPU_MAX_HW_QUEUES", "")
     if not cur and not _hip_initialised():
         os.environ["GPU_MAX_HW_QUEUES"] = cur = str(want)
-    return int(cur) if cur.isdigit() and int(cur) > 0 else 4
+    return min(int(cur), 32) if cur.isdigit() and int(cur) > 0 else 4
 
 
 HW_QUEUES = _hw_queues()

@@ -13,7 +13,10 @@ from . import _build
 
 _lib = None
 
-ABI_VERSION = 6  # include/pt_abi.h PT_ABI_VERSION
+ABI_VERSION = 7  # include/pt_abi.h PT_ABI_VERSION
+# an older tuning build (tools/tune.py A/B against a previous round's library) loads when its structs
+# match: ABI 7 only added pt_unpack_ranks, which such a build does not have
+ABI_STRUCTS_SINCE = 6
 c_float_p = C.POINTER(C.c_float)
 c_double_p = C.POINTER(C.c_double)
 c_int_p = C.POINTER(C.c_int)
@@ -81,6 +84,7 @@ SIGNATURES = {
     "pt_owned_pixel_count": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int64)]),
     "pt_pack_owned": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pt_unpack_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "pt_unpack_ranks": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     "pt_display_pack": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_void_p]),
     "pt_display_own": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_void_p]),
     "pt_display_unpack": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.c_void_p]),
@@ -160,12 +164,19 @@ def load(build_if_missing: bool = False):
         _build.build_native()
     _share_torch_hip_runtime()
     lib = C.CDLL(str(path))
+    lib.pt_abi_version.restype = C.c_int
+    abi = lib.pt_abi_version()
+    older_variant = _variant is not None and ABI_STRUCTS_SINCE <= abi < ABI_VERSION
+    if abi != ABI_VERSION and not older_variant:  # the structs below must match the library's
+        raise RuntimeError(f"{path} has ABI {abi}, this binding {ABI_VERSION}: rebuild it")
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if older_variant:
+                continue
+            raise RuntimeError(f"{path} does not export {name}: rebuild it")
         fn.restype = res
         fn.argtypes = args
-    if lib.pt_abi_version() != ABI_VERSION:  # the structs below must match the library's
-        raise RuntimeError(f"{path} has ABI {lib.pt_abi_version()}, this binding {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

@@ -258,12 +258,13 @@ struct PackParams {
   int width, height, shardSize, shardsX, rank, world;
   long count;
 };
-// the displayed frame's unpack on rank 0 (pt_display_unpack): ranks 1..world-1's packed RGB8
-// buffers (null: skipped) and slot counts; base's rank / count are per rank
+// rank 0's unpack of ranks 1..world-1's packed buffers in one launch (pt_display_unpack: RGB8
+// display values; pt_unpack_ranks: f32 running means); null buffers are skipped; base's rank /
+// count are per rank
 constexpr int DISPLAY_MAX_WORLD = 16;
-struct DisplayUnpack {
+struct RanksUnpack {
   PackParams base;
-  const uint8_t* src[DISPLAY_MAX_WORLD];
+  const void* src[DISPLAY_MAX_WORLD];
   long count[DISPLAY_MAX_WORLD];
 };
 
@@ -365,7 +366,8 @@ hipError_t launchDisplayPack(const PackParams& p, const float4* accum, float lim
                              hipStream_t s);
 hipError_t launchDisplayOwn(const PackParams& p, const float4* accum, float limit, float gamma, uchar4* image,
                             hipStream_t s);
-hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image, hipStream_t s);
+hipError_t launchDisplayUnpack(const RanksUnpack& d, int world, uchar4* image, hipStream_t s);
+hipError_t launchUnpackRanks(const RanksUnpack& d, int world, float4* accum, hipStream_t s);
 hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed, hipStream_t s);
 // the running-mean updates of nFrames pipelined frames over the rank's owned pixels (PackParams
 // mapping), in frame order: for f = 0 .. nFrames-1, accum = mix(accum, col + f * colStride,

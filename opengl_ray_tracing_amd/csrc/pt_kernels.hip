@@ -1090,9 +1090,9 @@ __global__ void displayOwnKernel(PackParams p, const float4* accum, float limit,
   image[i] = make_uchar4((uint8_t)unorm8(c.x), (uint8_t)unorm8(c.y), (uint8_t)unorm8(c.z), 255);
 }
 // blockIdx.y = rank - 1 of ranks 1..world-1 (their packed buffers in d.src)
-__global__ void displayUnpackKernel(DisplayUnpack d, uchar4* image) {
+__global__ void displayUnpackKernel(RanksUnpack d, uchar4* image) {
   const int rank = blockIdx.y + 1;
-  const uint8_t* src = d.src[rank];
+  const uint8_t* src = static_cast<const uint8_t*>(d.src[rank]);
   if (!src) return;
   PackParams p = d.base;
   p.rank = rank;
@@ -1102,6 +1102,22 @@ __global__ void displayUnpackKernel(DisplayUnpack d, uchar4* image) {
   int px, py;
   if (packedPixel(p, k, px, py))
     image[(size_t)py * p.width + px] = make_uchar4(src[3 * k], src[3 * k + 1], src[3 * k + 2], 255);
+}
+
+// unpackKernel of ranks 1..world-1 in one launch (blockIdx.y = rank - 1): rank 0's reassembly of
+// a gather of the f32 running means after each batch of frames
+__global__ void unpackRanksKernel(RanksUnpack d, float4* accum) {
+  const int rank = blockIdx.y + 1;
+  const float* src = static_cast<const float*>(d.src[rank]);
+  if (!src) return;
+  PackParams p = d.base;
+  p.rank = rank;
+  p.count = d.count[rank];
+  long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= p.count) return;
+  int px, py;
+  if (packedPixel(p, k, px, py))
+    accum[(size_t)py * p.width + px] = make_float4(src[3 * k], src[3 * k + 1], src[3 * k + 2], 1.0f);
 }
 
 // the running means of a batch of pipelined frames (accumulate's update, deferred to frame
@@ -1255,7 +1271,15 @@ hipError_t launchDisplayOwn(const PackParams& p, const float4* accum, float limi
                      gamma, image);
   return hipGetLastError();
 }
-hipError_t launchDisplayUnpack(const DisplayUnpack& d, int world, uchar4* image, hipStream_t s) {
+hipError_t launchUnpackRanks(const RanksUnpack& d, int world, float4* accum, hipStream_t s) {
+  long most = 0;
+  for (int k = 1; k < world; k++) most = d.count[k] > most ? d.count[k] : most;
+  if (world < 2 || most <= 0) return hipSuccess;
+  hipLaunchKernelGGL(unpackRanksKernel, dim3((unsigned)((most + 255) / 256), (unsigned)(world - 1)), dim3(256), 0, s,
+                     d, accum);
+  return hipGetLastError();
+}
+hipError_t launchDisplayUnpack(const RanksUnpack& d, int world, uchar4* image, hipStream_t s) {
   long most = 0;
   for (int k = 1; k < world; k++) most = d.count[k] > most ? d.count[k] : most;
   if (world < 2 || most <= 0) return hipSuccess;

@@ -295,6 +295,7 @@ template <int INTEG, bool CULL, int WAVES = 0, bool W4 = false, int BS = BLOCK, 
 __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_WAVES_MIS : PT_REGEN_MIN_WAVES_U)) void regenKernel(
     RenderParams p) {
   static_assert(!FULL || W4, "the LDS tree is the 4-wide one");
+  static_assert(!FULL || PT_REGEN_YIELD > 0, "the whole LDS tree is walked by walk4Run (loadNode4Lds) only");
   constexpr bool TILE_PRIM = PT_TILE_PRIM && INTEG != 2;
   __shared__ int s_stack[REGEN_LDS_STACK * BS];
   StackT<REGEN_LDS_STACK, BS> st;
@@ -596,7 +597,7 @@ constexpr int FULL_BS = 256 * PT_WIDE_REGEN_WAVES_U;  // one block per CU: all i
 constexpr size_t LDS_BYTES = 160 * 1024;
 template <int I>
 static const void* regenFn(bool cull, bool wide, bool full) {
-  if constexpr (I != 2)  // the uniform integrators' variant only
+  if constexpr (I != 2 && PT_REGEN_YIELD > 0)  // the uniform integrators' variant only
     if (full) return (const void*)regenKernel<I, true, wideRegenWaves(I), true, FULL_BS, true>;
   if (wide) return (const void*)regenKernel<I, true, wideRegenWaves(I), true>;
   return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
@@ -606,24 +607,36 @@ static const void* regenFnI(int integrator, bool cull, bool wide, bool full) {
                                                                          : regenFn<2>(cull, wide, full);
 }
 
+static long long fullStaticLds(int integrator) {
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, regenFnI(integrator, true, true, true)) != hipSuccess) return -1;
+  return (long long)fa.sharedSizeBytes;
+}
+
 hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenShape* out) {
   RegenShape r;
   r.wide = wide && cull;
   const size_t treeBytes = (size_t)f4nDev * W4_LDS_F4 * sizeof(float4);
-  const size_t staticBytes = (size_t)REGEN_LDS_STACK * FULL_BS * sizeof(int) + 2 * sizeof(float4) +
-                             (PT_PHASE_STATS ? (size_t)FULL_BS / 64 * 16 * sizeof(unsigned long long) : 0);
-  r.fullTree = PT_LDS_TREE && r.wide && integrator != 2 && f4nDev > 0 &&
+  // the FULL variant's static LDS (stack rows, hand-out rows, phase counters) as compiled
+  // (a property of the code object, the same on every device: read once per integrator)
+  size_t staticBytes = 0;
+  if (PT_LDS_TREE && PT_REGEN_YIELD > 0 && r.wide && integrator != 2 && f4nDev > 0) {
+    static const long long cached[2] = {fullStaticLds(0), fullStaticLds(1)};
+    if (cached[integrator] < 0) return hipErrorInvalidDeviceFunction;
+    staticBytes = (size_t)cached[integrator];
+  }
+  // the whole tree in LDS needs the resumable walk (walk4Run's ALL records): with PT_REGEN_YIELD = 0
+  // the walks run traceRay4, which reads an LDS top at the built 8-float4 stride
+  r.fullTree = PT_LDS_TREE && PT_REGEN_YIELD > 0 && r.wide && integrator != 2 && f4nDev > 0 &&
                treeBytes + staticBytes <= LDS_BYTES;
   r.block = r.fullTree ? FULL_BS : BLOCK;
   r.dynLds = r.fullTree ? treeBytes : 0;
   const void* f = regenFnI(integrator, cull, r.wide, r.fullTree);
-  if (r.fullTree) {  // once per kernel: room for any tree that fits beside the stacks
-    static bool granted[3] = {false, false, false};
-    if (!granted[integrator]) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BYTES - staticBytes));
-      if (e != hipSuccess) return e;
-      granted[integrator] = true;
-    }
+  if (r.fullTree) {
+    // room for any tree that fits beside the static LDS; a function attribute is per device, and
+    // setting it is cheap, so every shape query on the current device sets it
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BYTES - staticBytes));
+    if (e != hipSuccess) return e;
   }
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&r.blocksPerCU, f, r.block, r.dynLds);
   *out = r;
@@ -632,7 +645,7 @@ hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenSha
 
 template <int I>
 static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, bool cull, const RegenShape& r) {
-  if constexpr (I != 2) {
+  if constexpr (I != 2 && PT_REGEN_YIELD > 0) {
     if (r.fullTree) {
       hipLaunchKernelGGL((regenKernel<I, true, wideRegenWaves(I), true, FULL_BS, true>), dim3(grid), dim3(FULL_BS),
                          r.dynLds, s, p);

@@ -1983,14 +1983,30 @@ int pt_display_unpack(pt_ctx* ctx, int world, const void* const* dpacked, void* 
   if (!ctx || !dpacked || !dimage || world < 1 || world > DISPLAY_MAX_WORLD) return PT_E_INVALID;
   if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
   CK(hipSetDevice(ctx->cfg.device_id));
-  DisplayUnpack d;
+  RanksUnpack d;
   std::memset(&d, 0, sizeof(d));
   d.base = packParams(ctx, 0, world);
   for (int k = 1; k < world; k++) {
-    d.src[k] = reinterpret_cast<const uint8_t*>(dpacked[k]);
+    d.src[k] = dpacked[k];
     d.count[k] = packParams(ctx, k, world).count;
   }
   CK(launchDisplayUnpack(d, world, reinterpret_cast<uchar4*>(dimage), ctx->stream));
+  return PT_OK;
+}
+
+int pt_unpack_ranks(pt_ctx* ctx, int world, const void* const* dpacked) {
+  if (!ctx || !dpacked || world < 1 || world > DISPLAY_MAX_WORLD) return PT_E_INVALID;
+  if (!ctx->peers.empty()) return fail(ctx, PT_E_INVALID, "device groups gather inside pt_render_frame");
+  if (int rc = joinPipe(ctx)) return rc;
+  CK(hipSetDevice(ctx->cfg.device_id));
+  RanksUnpack d;
+  std::memset(&d, 0, sizeof(d));
+  d.base = packParams(ctx, 0, world);
+  for (int k = 1; k < world; k++) {
+    d.src[k] = dpacked[k];
+    d.count[k] = packParams(ctx, k, world).count;
+  }
+  CK(launchUnpackRanks(d, world, ctx->d_accum, ctx->stream));
   return PT_OK;
 }
 

@@ -76,8 +76,8 @@ class FrameGather:
       (pt_display_own / pt_display_unpack). A quarter of the accumulation's bytes cross
       xGMI per frame; each rank's running mean stays with it (`gather_accum()` brings the
       whole accumulation to rank 0 when it is wanted, bit-identical to a 1-GPU render).
-    * "accum" -- the running mean itself (3 f32 per pixel, pt_pack_owned / pt_unpack_rank)
-      into rank 0's accumulation every frame.
+    * "accum" -- the running mean itself (3 f32 per pixel, pt_pack_owned / pt_unpack_ranks: the
+      other ranks' buffers in one launch) into rank 0's accumulation after every batch of frames.
 
     Device buffers are torch tensors (torch is the allocator/collective plumbing here).
     The renderer runs on a torch stream of its own; each call packs the frame just
@@ -90,18 +90,22 @@ class FrameGather:
     """
 
     def __init__(self, renderer, rank: int, world: int, device, overlap: bool = True, mode: str = "accum",
-                 limit: float = 1.5, gamma: float = 0.0):
+                 limit: float = 1.5, gamma: float = 0.0, proxy: bool = False):
+        """proxy: one process on one GPU times rank `rank`'s share of the split with its real
+        per-batch work -- the pack, and on rank 0 the unpack of every other rank's buffer -- but
+        no collective (the receive buffers keep what they hold; tools/shard_time.py)."""
         import torch
         import torch.distributed as dist
 
         if mode not in ("accum", "display"):
             raise ValueError(f"mode {mode!r}")
         self.torch, self.dist = torch, dist
+        self.proxy = proxy
         self.r, self.rank, self.world, self.device = renderer, rank, world, device
         self.mode, self.limit, self.gamma = mode, float(limit), float(gamma)
         counts = [renderer.owned_pixel_count(k, world) for k in range(world)]
         self.maxc = max(counts)
-        self.overlap = overlap and not _staged()
+        self.overlap = overlap and (proxy or not _staged())
         # the renderer gets a stream of its own that torch knows about (torch's default
         # stream has the handle 0, which pt_set_stream reads as "the context's own stream")
         self.render_stream = torch.cuda.Stream(device)
@@ -143,9 +147,8 @@ class FrameGather:
     def _unpack(self, i):
         if self.mode == "display":
             self.r.display_unpack(self.world, self._recv_ptrs, self.images[i].data_ptr())
-        else:
-            for k in range(1, self.world):
-                self.r.unpack_rank(k, self.world, self.recv[k].data_ptr())
+        else:  # every other rank's running means in one launch (pt_unpack_ranks)
+            self.r.unpack_ranks(self.world, self._recv_ptrs)
 
     def __call__(self):
         torch, dist = self.torch, self.dist
@@ -156,7 +159,7 @@ class FrameGather:
         self._pack(i)  # on the render stream, after the frame
         if self.mode == "display" and self.rank == 0:
             self.last = i
-        if _staged():  # gloo rehearsal: the collective on host copies, ordered after the pack
+        if not self.proxy and _staged():  # gloo rehearsal: the collective on host copies, ordered after the pack
             with torch.cuda.stream(self.render_stream):
                 host = self.send[i].cpu()
                 recv = [torch.zeros_like(host) for _ in range(self.world)] if self.rank == 0 else None
@@ -169,7 +172,8 @@ class FrameGather:
         self.packed[i].record(self.render_stream)
         with torch.cuda.stream(self.comm_stream):
             self.comm_stream.wait_event(self.packed[i])
-            dist.gather(self.send[i], gather_list=self.recv, dst=0)
+            if not self.proxy:
+                dist.gather(self.send[i], gather_list=self.recv, dst=0)
             if self.rank == 0:
                 self.r.set_stream(self.comm_stream.cuda_stream)
                 self._unpack(i)
@@ -197,8 +201,7 @@ class FrameGather:
             else:
                 dist.gather(buf, gather_list=recv, dst=0)
             if self.rank == 0:
-                for k in range(1, self.world):
-                    self.r.unpack_rank(k, self.world, recv[k].data_ptr())
+                self.r.unpack_ranks(self.world, [0] + [t.data_ptr() for t in recv[1:]])
         self.render_stream.synchronize()
 
     def synchronize(self):

@@ -275,6 +275,12 @@ class Renderer:
     def unpack_rank(self, rank: int, world: int, dptr: int):
         self._ck(self._lib.pt_unpack_rank(self._h, int(rank), int(world), C.c_void_p(dptr)), "pt_unpack_rank")
 
+    def unpack_ranks(self, world: int, dpacked):
+        """Ranks 1..world-1's packed running means (device pointers, entry 0 ignored) into the
+        accumulation, one launch."""
+        arr = (C.c_void_p * world)(*[C.c_void_p(int(x)) if x else C.c_void_p() for x in dpacked])
+        self._ck(self._lib.pt_unpack_ranks(self._h, int(world), arr), "pt_unpack_ranks")
+
     def display_pack(self, dptr: int, limit: float = 1.5, gamma: float = 0.0):
         """This rank's owned pixels of the displayed frame (pass3 into an 8-bit window), 3 u8 each."""
         self._ck(self._lib.pt_display_pack(self._h, float(limit), float(gamma), C.c_void_p(dptr)), "pt_display_pack")

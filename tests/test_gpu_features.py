@@ -181,8 +181,13 @@ def test_tile_shards_reassemble_bit_exact(world):
         r.synchronize()
         assert np.array_equal(t.cpu().numpy(), D.pack(ref, k, world)[:, :3])
         bufs.append(t)
+    rank0 = ranks[0].accum()
     for k in range(1, world):
         ranks[0].unpack_rank(k, world, bufs[k].data_ptr())
+    assert np.array_equal(ranks[0].accum(), ref)
+    # the same reassembly in one launch (pt_unpack_ranks, FrameGather's accum mode)
+    ranks[0].set_accum(rank0)
+    ranks[0].unpack_ranks(world, [0] + [b.data_ptr() for b in bufs[1:]])
     assert np.array_equal(ranks[0].accum(), ref)
     assert rays == total_rays
     for r in ranks:

@@ -2,10 +2,14 @@
 """Per-rank frame time of the screen-tile split, measured on one GPU: rank 0's
 share of an N-way split (its 32x32 tiles t % N == 0) rendered alone, wall ms per
 frame with frames in flight and frames batched per launch (pt_render_frames_async,
-PT_BATCH frames per launch, 0 = the renderer's choice; PT_BATCH_MUL = m: m x N). The N-GPU frame is at
-least this plus whatever of the per-batch gather does not overlap the next batch.
+PT_BATCH frames per launch, 0 = the renderer's choice; PT_BATCH_MUL = m: m x N), issued
+exactly as bench.py issues them -- batches of the renderer's frames per launch, each followed
+by rank 0's real per-batch work (distributed.FrameGather(proxy=True): the pack of its own tiles
+on the render stream, and the one-launch unpack of the other N - 1 ranks' buffers into its
+accumulation on the communication stream) but no collective (PT_SHARD_GATHER=0: render only).
+The N-GPU frame is this plus whatever of the xGMI gather itself does not overlap the next batch.
 
-    [PT_VARIANT=<tuning build>] [PT_BATCH=b | PT_BATCH_MUL=m] python tools/shard_time.py [config] [N ...]
+    [PT_VARIANT=<tuning build>] [PT_BATCH=b | PT_BATCH_MUL=m] [PT_SHARD_FRAMES=K] python tools/shard_time.py [config] [N ...]
 """
 import json
 import sys
@@ -14,11 +18,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
-# the bench's hardware queues (bench.py): 12, so the frames in flight get a queue each
-import os  # noqa: E402
-if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 12:
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
-
+# hardware queues: the package's policy (opengl_ray_tracing_amd/__init__.py), as bench.py and the tests
 import opengl_ray_tracing_amd  # noqa: E402,F401
 
 
@@ -36,19 +36,37 @@ def main():
     eye, rot = orbit_camera(*cfg.camera)
     batch = int(os.environ.get("PT_BATCH", "0"))
     mul = int(os.environ.get("PT_BATCH_MUL", "0"))  # frames per launch = mul x N (overrides PT_BATCH)
+    from opengl_ray_tracing_amd.distributed import FrameGather
+    with_gather = os.environ.get("PT_SHARD_GATHER", "1") != "0"
     for n in worlds:
         with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, tile_rank=0,
                       tile_world=n, frame_batch=mul * n if mul else batch) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
-            r.render_frames(eye, rot, 0, 100)  # policy probe (tree, split, order) + warmup
+            g = FrameGather(r, 0, n, "cuda:0", mode="accum", proxy=True) if with_gather and n > 1 else None
+            per = r.stats().frame_batch
+
+            def frames(first, k):  # bench.py's frames(): batches, each followed by the gather
+                while k > 0:
+                    m = min(per, k)
+                    r.render_frames(eye, rot, first, m)
+                    if g is not None:
+                        g()
+                    first += m
+                    k -= m
+
+            frames(0, 100)  # policy probe (tree, split, order) + warmup
             r.synchronize()
+            if g is not None:
+                g.synchronize()
             r.reset_stats()
             K = int(os.environ.get("PT_SHARD_FRAMES", "200"))  # 20: the driver's bench line, from an idle GPU
             t0 = time.perf_counter()
-            r.render_frames(eye, rot, 100, K)
+            frames(100, K)
             t_sub = time.perf_counter()
             r.synchronize()
+            if g is not None:
+                g.synchronize()
             ms = 1e3 * (time.perf_counter() - t0) / K
             submit_ms = 1e3 * (t_sub - t0) / K  # host time per pt_render_frame_async call
             st = r.stats()
@@ -56,7 +74,8 @@ def main():
                           "frames": st.frames, "launches": st.launches, "frame_batch": st.frame_batch,
                           "kernel_ms_avg": round(st.kernel_ms_total / max(st.launches, 1), 4),
                           "host_submit_ms": round(submit_ms, 4),
-                          "rays_per_frame": st.rays // max(st.frames, 1),
+                          "rays_per_frame": st.rays // max(st.frames, 1), "gather": g is not None,
+                          "hw_queues": opengl_ray_tracing_amd.HW_QUEUES,
                           "frames_in_flight": st.frames_in_flight}), flush=True)
 
 

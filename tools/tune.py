@@ -21,10 +21,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
-# the bench's hardware queues (bench.py): 12, so the frames in flight get a queue each
-import os  # noqa: E402
-if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 12:
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+# hardware queues: the package's policy (12 when GPU_MAX_HW_QUEUES is unset, an explicit value
+# respected), as bench.py and the tests
+import opengl_ray_tracing_amd  # noqa: E402,F401
 
 
 def child(variant: str, config: str, frames: int, warmup: int, builder, flags: int = 0, max_bounce=None):
@@ -49,6 +48,7 @@ def child(variant: str, config: str, frames: int, warmup: int, builder, flags: i
     ms = st.kernel_ms_total / st.launches
     # frames in flight overlap their launches: wall ms per frame is the comparable figure
     print(json.dumps({"variant": variant, "flags": flags, "config": config, "max_bounce": mb, "kernel_ms": round(ms, 4),
+                      "hw_queues": opengl_ray_tracing_amd.HW_QUEUES,
                       "wall_ms": round(wall, 4),
                       "rays": st.rays // max(st.frames, 1), "frames_per_launch": st.frame_batch,
                       "mrays_s": round(st.rays / (st.kernel_ms_total * 1e-3) / 1e6, 1)}), flush=True)
