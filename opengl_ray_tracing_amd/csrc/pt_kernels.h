@@ -187,7 +187,9 @@ struct RenderParams {
   float4* col;
   // A batch of nFrames consecutive frames of one camera in this launch (pt_render_frames_async):
   // frame f draws sample index sampleIndex + f * sampleStride and writes its colours to
-  // col + f * colStride (pixels) and its camera-ray results to primHit + f * colStride. Work
+  // col + f * colStride and its camera-ray results to primHit + f * colStride, each indexed by the
+  // pixel's slot in this context's screen-tile share (shareIndex: the packed order of
+  // pt_pack_owned; colStride = the share's slots), so a 1/N share's buffers are 1/N of a frame. Work
   // item k of the launch is item k / nFrames of frame k % nFrames, so the frames of one tile
   // run side by side (the same camera rays, the same nodes). nFrames 1: a single frame.
   int nFrames;

@@ -274,7 +274,7 @@ __device__ __forceinline__ void accumulate(const RenderParams& p, const FrameRef
                                            bool count) {
   float4* col = f.col;
   if (!count && col) {  // pipelined frame: the sample colour, mixed into the running mean in frame order (mixKernel)
-    stStream(col + (size_t)py * p.width + px, make_float4(color.x, color.y, color.z, 1.0f));
+    stStream(col + shareIndex(p, px, py), make_float4(color.x, color.y, color.z, 1.0f));
     return;
   }
   float4* a = p.accum + (size_t)py * p.width + px;
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
     b1 = p.binStart[ty * p.binTilesX + tx + 1];
   }
   const int n = b1 - b0;
-  int2* out = p.primHit + (size_t)fr * p.colStride + (size_t)py * p.width + px;
+  int2* out = p.primHit + (size_t)fr * p.colStride + shareIndex(p, px, py);
   FrameRef fp;  // this block's frame (accumulate's colour buffer)
   fp.col = p.col ? p.col + (size_t)fr * p.colStride : nullptr;
   fp.sampleIndex = p.sampleIndex + (uint32_t)fr * p.sampleStride;
@@ -918,7 +918,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
     const bool valid = lane < nLanes && px < p.width && py < p.height;
     if (!COUNT && p.primHit) {  // camera rays already traced by primaryKernel
-      const int2 h = valid ? p.primHit[(size_t)fr * p.colStride + (size_t)py * p.width + px] : make_int2(PRIM_MISS, 0);
+      const int2 h = valid ? p.primHit[(size_t)fr * p.colStride + shareIndex(p, px, py)] : make_int2(PRIM_MISS, 0);
       int tri = h.x;
       float t = __int_as_float(h.y);
       if (__ballot(valid && tri == PRIM_TILE)) {  // wave-uniform: the whole tile
@@ -1132,7 +1132,7 @@ __global__ void mixKernel(PackParams p, float4* accum, const float4* col, size_t
   const size_t i = (size_t)py * p.width + px;
   float4 a = ldStream(accum + i);
   for (int f = 0; f < nFrames; f++) {
-    const float4 c = ldStream(col + (size_t)f * colStride + i);
+    const float4 c = ldStream(col + (size_t)f * colStride + k);  // slot k of the share (shareIndex)
     const float w = 1.0f / (float)(frameCounter + (uint32_t)f + 1u);
     a = make_float4(mixf(a.x, c.x, w), mixf(a.y, c.y, w), mixf(a.z, c.z, w), 1.0f);
   }

@@ -95,7 +95,7 @@ __device__ __forceinline__ uint32_t sampleOf(const RenderParams& p, const PathSt
 __device__ __forceinline__ void writeAccum(const RenderParams& p, const PathState& s, V3 color) {
   const int px = s.px, py = s.py;
   if (p.col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in frame order
-    stStream(p.col + (size_t)s.fr * p.colStride + (size_t)py * p.width + px,
+    stStream(p.col + (size_t)s.fr * p.colStride + shareIndex(p, px, py),
              make_float4(color.x, color.y, color.z, 1.0f));
     return;
   }
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
             const bool in = px < p.width && py < p.height;
             // without the camera-ray pass every pixel's camera ray is traced here (PRIM_RETRACE)
             const int2 h = !in ? make_int2(PRIM_MISS, 0)
-                               : p.primHit ? p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px]
+                               : p.primHit ? p.primHit[(size_t)tileFr * p.colStride + shareIndex(p, px, py)]
                                            : make_int2(PRIM_RETRACE, 0);
             const unsigned long long valid = __ballot(h.x != PRIM_MISS);
             if (h.x != PRIM_MISS) {
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
           const int py = tilePy(p, tile, sub) + (slot >> 3);
           int2 h = make_int2(0, 0);
           if (p.primHit && px < p.width && py < p.height)
-            h = p.primHit[(size_t)tileFr * p.colStride + (size_t)py * p.width + px];
+            h = p.primHit[(size_t)tileFr * p.colStride + shareIndex(p, px, py)];
           if (px < p.width && py < p.height && !(p.primHit && h.x == PRIM_MISS)) {
             s.px = px;
             s.py = py;

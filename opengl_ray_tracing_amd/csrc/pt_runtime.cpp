@@ -151,6 +151,8 @@ struct pt_ctx {
   // frames in flight (PIPE slots; see PIPE above)
   bool pipe = false;                        // this context pipelines its megakernel frames
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
+  int spreadLeft = 0;                       // pt_render_frames_async: launches of the call still to issue,
+                                            // this one included (0: not spreading; grid shares, renderOne)
   int pipeDepthBase = PT_PIPE;              // ... as chosen at creation (uploadScene may lower it for large scenes)
   bool pipeDepthFixed = false;              // PT_PIPE_DEPTH set: no scene-dependent choice
   // Frames of one pt_render_frames_async call rendered per launch (RenderParams::nFrames), at most:
@@ -1521,7 +1523,11 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     for (int k = 0; k < D; k++)
       others += k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
     (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
-    if (others > 0) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * (others + 1))));
+    // a call spread over several launches (pt_render_frames_async) counts the ones it has yet to issue
+    // too, so the first of them does not take the whole machine from the rest
+    const int coming = std::max(1, ctx->spreadLeft);
+    if (others + coming > 1)
+      grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * (others + coming))));
   }
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)fullGrid * bs, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
@@ -1600,14 +1606,18 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   if (done) *done = nF;
   p.nFrames = nF;
   p.sampleStride = c.sample_world > 0 ? (uint32_t)c.sample_world : 1u;
-  p.colStride = npix;
+  // per-frame buffers indexed by the pixel's slot in this context's share (shareIndex): a 1/N share's
+  // colour and camera-ray buffers are 1/N of a frame (c5 at N = 8, 16 frames per launch: ~2.4 GB of
+  // colour buffers instead of ~19 GB)
+  const size_t shareN = (size_t)ctx->numItems * 64;
+  p.colStride = shareN;
   if (piped && ctx->colCap[colIdx] < nF) {  // room for the launch's frames (each buffer grows once, to batchCap)
     if (ctx->d_col[colIdx]) {
       CK(hipEventSynchronize(ctx->mixDone[colIdx]));  // its last frames' running-mean update has read it
       dfree(ctx->d_col[colIdx]);
     }
     const int cap = std::max(nF, ctx->batchCap);
-    CK(hipMalloc(&ctx->d_col[colIdx], (size_t)cap * npix * sizeof(float4)));
+    CK(hipMalloc(&ctx->d_col[colIdx], (size_t)cap * shareN * sizeof(float4)));
     ctx->colCap[colIdx] = cap;
   }
   p.col = piped ? ctx->d_col[colIdx] : nullptr;
@@ -1655,7 +1665,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
           dfree(ctx->d_prim[slot]);
         }
         const int cap = std::max(nF, piped ? ctx->batchCap : 1);
-        CK(hipMalloc(&ctx->d_prim[slot], (size_t)cap * npix * sizeof(int2)));
+        CK(hipMalloc(&ctx->d_prim[slot], (size_t)cap * shareN * sizeof(int2)));
         ctx->primCap[slot] = cap;
       }
       p.primHit = ctx->d_prim[slot];
@@ -1722,7 +1732,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     if (ctx->mixPending && ctx->lastMixStream != ctx->stream)  // the caller switched streams: keep frame order
       CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastCol], 0));
     ctx->lastMixStream = ctx->stream;
-    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[colIdx], npix, nF,
+    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[colIdx], shareN, nF,
                  frameCounter, ctx->stream));
     CK(hipEventRecord(ctx->mixDone[colIdx], ctx->stream));
     ctx->lastSlot = slot;
@@ -1760,9 +1770,45 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   return pt_render_frames_async(ctx, eye, cameraRotate, frameCounter, 1);
 }
 
+// A call's frames spread over concurrent launches (PT_SPREAD = q > 0): launches of at least q / 4 of
+// an image's work each (frames of a tile_world share: q * tile_world / 4), at most the frames in
+// flight, every launch's grid a share of the machine from the first one on -- so a short request
+// from an idle GPU (the driver's 20-frame bench window; at N = 8 two calls of 16 + 4 frames) runs
+// its launches side by side and their tails overlap, instead of a first launch holding every CU
+// until its longest paths end.
+#ifndef PT_SPREAD_DEFAULT
+#define PT_SPREAD_DEFAULT 0
+#endif
+static int spreadLaunches(const pt_ctx* ctx, int nFrames) {
+  static const int q = [] {
+    const char* e = std::getenv("PT_SPREAD");
+    return e ? std::max(0, std::atoi(e)) : PT_SPREAD_DEFAULT;
+  }();
+  if (q <= 0 || !ctx->pipe || nFrames < 2) return 1;
+  const int minF = std::max(1, q * std::max(1, ctx->cfg.tile_world) / 4);
+  return std::max(1, std::min(nFrames / minF, ctx->pipeDepth));
+}
+
 int pt_render_frames_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter,
                            int nFrames) {
   if (!ctx || nFrames < 0) return PT_E_INVALID;
+  const int L = ctx->peers.empty() ? spreadLaunches(ctx, nFrames) : 1;
+  if (L > 1) {  // L launches of (nearly) equal frames, issued back to back
+    for (int k = 0; k < L && nFrames > 0; k++) {
+      int per = (nFrames + (L - k) - 1) / (L - k);
+      while (per > 0) {
+        int done = 1;
+        ctx->spreadLeft = L - k;
+        const int rc = renderOne(ctx, eye, cameraRotate, frameCounter, per, &done);
+        ctx->spreadLeft = 0;
+        if (rc) return rc;
+        frameCounter += (uint32_t)done;
+        nFrames -= done;
+        per -= done;
+      }
+    }
+    return PT_OK;
+  }
   while (nFrames > 0) {
     int done = 1;
     if (ctx->peers.empty()) {

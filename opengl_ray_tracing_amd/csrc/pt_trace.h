@@ -160,6 +160,8 @@ __device__ __forceinline__ float clampInv(float v) { return copysignf(fminf(fabs
 // faster everywhere (c2 0.2122 -> 0.2056 ms, c4 0.2926 -> 0.2775, c5 5.59 -> 5.51; spills of
 // the MIS kernels 28 -> 13 and 88 -> 76 VGPRs). The same IEEE fma, so the same results.
 __device__ __forceinline__ f32x2 fmaBcast(f32x2 a, f32x2 s) {
+  // (v_pk_fma_f32 with op_sel broadcasting s's halves, as inline asm, halves these FMAs but makes the
+  // compiler canonicalise every result before the IEEE-mode min/max: 24 v_max added, not kept)
   return f32x2{__builtin_fmaf(a.x, s.x, s.y), __builtin_fmaf(a.y, s.x, s.y)};
 }
 __device__ __forceinline__ FusedRay fusedRay(V3 o, V3 inv) {
@@ -530,6 +532,9 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
 }
 
 // ----------------------------------------------------------------- resumable 4-wide walk
+#ifndef PT_LEAF_WAIT
+#define PT_LEAF_WAIT 0
+#endif
 // traceRay4 as a walk that can stop and resume (the regen kernel's dynamic ray
 // fetch, PT_REGEN_YIELD): the walk's state is a Walk4 plus the lane's stack, and
 // walk4Run returns once the lane's walk is done -- or, for the whole wave, as
@@ -620,7 +625,9 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
         next = st.sp > 0 ? st.pop() : REF_NONE;
       }
       w.ref = next;
-      if (__ballot(w.leaf == REF_NONE) == 0) break;
+      // the node phase ends once at most PT_LEAF_WAIT of its lanes still look for a leaf (0: every
+      // lane holds one, traceRay's while-while); the few still looking go on after the leaf phase
+      if (__popcll(__ballot(w.leaf == REF_NONE)) <= PT_LEAF_WAIT) break;
     }
     if (w.leaf == REF_NONE && isLeafRef(w.ref)) {
       w.leaf = w.ref;
@@ -855,6 +862,16 @@ struct TileCursor {
     return -1;
   }
 };
+
+// Slot of pixel (px, py) in this context's screen-tile share, in the packed order of pt_pack_owned
+// (pt_kernels.hip packedPixel): the index of a pipelined frame's colour and camera-ray buffers
+// (RenderParams::colStride slots per frame). (px, py) must be one of the share's pixels.
+__device__ __forceinline__ size_t shareIndex(const RenderParams& p, int px, int py) {
+  const int ss = p.shardSize;
+  const int gx = px / ss, gy = py / ss;
+  const int j = (gy * p.shardsX + gx) / p.world;  // the share's j-th shard tile
+  return (size_t)j * ss * ss + (size_t)((py - gy * ss) * ss + (px - gx * ss));
+}
 
 // per-wave sum of a lane counter into the block's padded shard
 __device__ __forceinline__ void addRays(unsigned long long* shards, uint32_t r) {
