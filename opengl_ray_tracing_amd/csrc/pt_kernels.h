@@ -130,6 +130,7 @@ struct SceneView {
   // floats 18..20, IS:207-232). 64 + ~0 bytes per triangle instead of 144.
   const float4* hitRec;
   const float4* mats;
+  int nMats;           // materials in mats
   const float4* bvh;   // 4 float4 per device node id (pt_runtime.cpp: top of the tree first, breadth-first)
   int nTop;            // device ids [0, nTop) are the top of the tree, staged in LDS by the megakernel
   int rootRef;         // encoded reference to node 1
@@ -147,9 +148,8 @@ struct SceneView {
   // traceRay4): W4_F4 float4 per node, breadth-first ids, leaves as in fbvh; null = none
   const float4* fbvh4;
   int f4Root, f4nTop;
-  // reference facts: each triangle's reference leaf (-1 = none) and that leaf's
-  // box (lo, hi), every reference node's parent and box (lo, hi)
-  const int* refLeafOf;
+  // reference facts: each triangle's reference leaf's box (lo, hi; lo.w = the leaf's node id as
+  // int bits, -1 = in no leaf), every reference node's parent and box (lo, hi)
   const int* refParent;
   const float4* refBox;
   const float4* leafBox;

@@ -103,7 +103,6 @@ struct pt_ctx {
   float4* d_fbvh = nullptr;
   float4* d_fpairs = nullptr;
   int* d_fastTri = nullptr;
-  int* d_refLeafOf = nullptr;
   int* d_refParent = nullptr;
   float4* d_refBox = nullptr;
   float4* d_leafBox = nullptr;
@@ -151,8 +150,6 @@ struct pt_ctx {
   // frames in flight (PIPE slots; see PIPE above)
   bool pipe = false;                        // this context pipelines its megakernel frames
   int pipeDepth = PT_PIPE;                  // frames in flight (slot streams in use), 1..PIPE
-  int spreadLeft = 0;                       // pt_render_frames_async: launches of the call still to issue,
-                                            // this one included (0: not spreading; grid shares, renderOne)
   int pipeDepthBase = PT_PIPE;              // ... as chosen at creation (uploadScene may lower it for large scenes)
   bool pipeDepthFixed = false;              // PT_PIPE_DEPTH set: no scene-dependent choice
   // Frames of one pt_render_frames_async call rendered per launch (RenderParams::nFrames), at most:
@@ -448,7 +445,7 @@ void pt_destroy(pt_ctx* ctx) {
   (void)hipSetDevice(ctx->cfg.device_id);
   if (ctx->own) (void)hipStreamSynchronize(ctx->own);
   dfree(ctx->d_geo); dfree(ctx->d_hit); dfree(ctx->d_mats); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
-  dfree(ctx->d_fbvh); dfree(ctx->d_fbvh4); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri); dfree(ctx->d_refLeafOf);
+  dfree(ctx->d_fbvh); dfree(ctx->d_fbvh4); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri);
   dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
   dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
@@ -799,6 +796,8 @@ static void prepareAccel(const float* tris, int nTri, const float* nodes, int nN
   }
   const float inf = INFINITY;
   for (int i = 0; i < nTri; i++) {
+    // lo.w holds the reference leaf's node id (int bits), so the reachability check reads one
+    // 32-byte record per hit instead of that record and a separate leaf-id array
     if (leafOf[i] < 0) {  // in no reference leaf: never a reference hit (empty box fails the margin test)
       h.leafBox[2 * (size_t)i] = make_float4(inf, inf, inf, 0.0f);
       h.leafBox[2 * (size_t)i + 1] = make_float4(-inf, -inf, -inf, 0.0f);
@@ -806,6 +805,8 @@ static void prepareAccel(const float* tris, int nTri, const float* nodes, int nN
       h.leafBox[2 * (size_t)i] = h.refBox[2 * (size_t)leafOf[i]];
       h.leafBox[2 * (size_t)i + 1] = h.refBox[2 * (size_t)leafOf[i] + 1];
     }
+    int id = leafOf[i];
+    std::memcpy(&h.leafBox[2 * (size_t)i].w, &id, sizeof(int));
   }
   // the tree itself: on the GPU by uploadScene (pt_build.hip), or here (scene.cpp's threaded binned SAH)
   if (!hostBuild) {
@@ -924,7 +925,7 @@ static int uploadScene(pt_ctx* ctx, const float* tris, const SceneHost& h) {
   ctx->accelMs = 0.0f;
   ctx->accelNodes = ctx->accelDepth = 0;
   if (!h.fast) return PT_OK;
-  if ((rc = upload(ctx, &ctx->d_refLeafOf, h.leafOf)) || (rc = upload(ctx, &ctx->d_refParent, h.parent)) ||
+  if ((rc = upload(ctx, &ctx->d_refParent, h.parent)) ||
       (rc = upload(ctx, &ctx->d_refBox, h.refBox)) || (rc = upload(ctx, &ctx->d_leafBox, h.leafBox)))
     return rc;
   if (h.deviceBuild) {
@@ -1273,6 +1274,7 @@ static SceneView sceneView(const pt_ctx* ctx) {
   s.pairs = ctx->d_pairs;
   s.hitRec = ctx->d_hit;
   s.mats = ctx->d_mats;
+  s.nMats = ctx->nMats;
   s.bvh = ctx->d_bvh;
   s.nTop = std::min(LDS_NODES, ctx->nDevNodes);
   s.rootRef = ctx->rootRef;
@@ -1286,7 +1288,6 @@ static SceneView sceneView(const pt_ctx* ctx) {
   s.fbvh4 = ctx->d_fbvh4;
   s.f4Root = ctx->f4Root;
   s.f4nTop = std::min(LDS_NODES * 4 / W4_F4, ctx->f4nDev);  // the LDS copy holds LDS_NODES * 4 float4
-  s.refLeafOf = ctx->d_refLeafOf;
   s.refParent = ctx->d_refParent;
   s.refBox = ctx->d_refBox;
   s.leafBox = ctx->d_leafBox;
@@ -1523,11 +1524,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     for (int k = 0; k < D; k++)
       others += k != slot && ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady;
     (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
-    // a call spread over several launches (pt_render_frames_async) counts the ones it has yet to issue
-    // too, so the first of them does not take the whole machine from the rest
-    const int coming = std::max(1, ctx->spreadLeft);
-    if (others + coming > 1)
-      grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * (others + coming))));
+    if (others > 0) grid = std::min(fullGrid, std::max(NUM_QUEUES, fullGrid * GRID_PCT / (100 * (others + 1))));
   }
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)fullGrid * bs, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
@@ -1770,45 +1767,9 @@ int pt_render_frame_async(pt_ctx* ctx, const float eye[3], const float cameraRot
   return pt_render_frames_async(ctx, eye, cameraRotate, frameCounter, 1);
 }
 
-// A call's frames spread over concurrent launches (PT_SPREAD = q > 0): launches of at least q / 4 of
-// an image's work each (frames of a tile_world share: q * tile_world / 4), at most the frames in
-// flight, every launch's grid a share of the machine from the first one on -- so a short request
-// from an idle GPU (the driver's 20-frame bench window; at N = 8 two calls of 16 + 4 frames) runs
-// its launches side by side and their tails overlap, instead of a first launch holding every CU
-// until its longest paths end.
-#ifndef PT_SPREAD_DEFAULT
-#define PT_SPREAD_DEFAULT 0
-#endif
-static int spreadLaunches(const pt_ctx* ctx, int nFrames) {
-  static const int q = [] {
-    const char* e = std::getenv("PT_SPREAD");
-    return e ? std::max(0, std::atoi(e)) : PT_SPREAD_DEFAULT;
-  }();
-  if (q <= 0 || !ctx->pipe || nFrames < 2) return 1;
-  const int minF = std::max(1, q * std::max(1, ctx->cfg.tile_world) / 4);
-  return std::max(1, std::min(nFrames / minF, ctx->pipeDepth));
-}
-
 int pt_render_frames_async(pt_ctx* ctx, const float eye[3], const float cameraRotate[16], uint32_t frameCounter,
                            int nFrames) {
   if (!ctx || nFrames < 0) return PT_E_INVALID;
-  const int L = ctx->peers.empty() ? spreadLaunches(ctx, nFrames) : 1;
-  if (L > 1) {  // L launches of (nearly) equal frames, issued back to back
-    for (int k = 0; k < L && nFrames > 0; k++) {
-      int per = (nFrames + (L - k) - 1) / (L - k);
-      while (per > 0) {
-        int done = 1;
-        ctx->spreadLeft = L - k;
-        const int rc = renderOne(ctx, eye, cameraRotate, frameCounter, per, &done);
-        ctx->spreadLeft = 0;
-        if (rc) return rc;
-        frameCounter += (uint32_t)done;
-        nFrames -= done;
-        per -= done;
-      }
-    }
-    return PT_OK;
-  }
   while (nFrames > 0) {
     int done = 1;
     if (ctx->peers.empty()) {
