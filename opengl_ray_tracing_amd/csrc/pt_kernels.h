@@ -72,7 +72,8 @@ constexpr int LDS_NODES = PT_LDS_NODES;
 // (refill, walk, reference check, shading; node and leaf iterations) -- tools/wave_trace.py --phases
 #define PT_PHASE_STATS 0
 #endif
-constexpr int WAVE_TRACE_WORDS = PT_PHASE_STATS ? 16 : 6;  // u64 per wave in RenderParams::waveTrace
+constexpr int PHASE_WORDS = 24;  // PT_PHASE_STATS record (pt_regen.hip)
+constexpr int WAVE_TRACE_WORDS = PT_PHASE_STATS ? PHASE_WORDS : 6;  // u64 per wave in RenderParams::waveTrace
  // traversal stack entries per lane kept in LDS (4 B x 256 lanes each)
 #ifndef PT_NUM_QUEUES
 #define PT_NUM_QUEUES 32

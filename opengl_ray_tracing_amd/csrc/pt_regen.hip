@@ -375,10 +375,12 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   // cycles, [2] reference-check cycles, [3] shading cycles, [4] main-loop iterations, [5] lanes
   // walking, [6] lanes shading, [7]/[8] node iterations / lanes, [9]/[10] pair tests / lanes,
   // [11] refill iterations, [12] lanes whose walk ran out of the yield, [13] walk calls that end
-  // every walk, [14] retraced lanes, [15] wave lifetime (clock64 cycles)
-  __shared__ unsigned long long s_ph[BS / 64][16];
+  // every walk, [14] retraced lanes, [15] wave lifetime (clock64 cycles); the TILE_PRIM hand-out:
+  // [16] hand-out cycles, [17] tile claims, [18] claim cycles (atomic + camera-ray results),
+  // [19] camera-hit shading cycles, [20] lanes shaded there, [21] camera-hit shading passes
+  __shared__ unsigned long long s_ph[BS / 64][PHASE_WORDS];
   unsigned long long* ph = s_ph[threadIdx.x >> 6];
-  if (lane < 16) ph[lane] = 0;
+  if (lane < PHASE_WORDS) ph[lane] = 0;
   const long long phStart = clock64();
 #define PH_ADD(k, x)                                                         \
   do {                                                                       \
@@ -406,13 +408,22 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
       while (true) {
         bool pend = false;
         int2 hP = make_int2(0, 0);
+#if PT_PHASE_STATS
+        const long long phH = clock64();
+#endif
         while (true) {
           PH_ADD(11, 1);
           const unsigned long long idle = __ballot(!active);
           if (idle == 0) break;
           if (cursor >= nValid) {
-            // (claiming the wave's next tile ahead, so the atomic overlaps the tile's paths, measured
-            // slower: c2 0.1807 -> 0.1841 ms, c5 4.25 -> 4.29 ms)
+#if PT_PHASE_STATS
+            const long long phC = clock64();
+            PH_ADD(17, 1);
+#endif
+            // (a claim -- the device-scope atomic, then the tile's camera-ray results -- is 1.6-2.3 us
+            // and 10-13 % of a c2 wave's time, PT_PHASE_STATS; measured slower: claiming the wave's
+            // next tile ahead, c2 0.1807 -> 0.1841 ms, c5 4.25 -> 4.29; 2 / 4 consecutive items per
+            // atomic, c2 0.2106 -> 0.2160 / 0.2390 at 4 hardware queues)
             const int item = cur.next(p.queue, p.perQueue, p.numItems, home, tileFr, p.nFrames);
             if (item < 0) {
               drained = true;
@@ -444,6 +455,9 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             nValid = __popcll(valid);
             cursor = 0;
+#if PT_PHASE_STATS
+            PH_ADD(18, clock64() - phC);
+#endif
             continue;  // an all-sky tile (nValid 0) is skipped without starting a path
           }
           const int r = cursor + rankBelow(idle);
@@ -461,6 +475,14 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
         }
         // the camera hits just taken, shaded together (a PRIM_RETRACE / PRIM_TILE camera ray is
         // traced below like any ray)
+#if PT_PHASE_STATS
+        PH_ADD(16, clock64() - phH);
+        const long long phS = clock64();
+        if (__ballot(pend)) {
+          PH_ADD(21, 1);
+          PH_ADD(20, __popcll(__ballot(pend)));
+        }
+#endif
         bool ended = false;
         if (pend) {
           startPath(p, s);
@@ -473,6 +495,9 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
             }
           }
         }
+#if PT_PHASE_STATS
+        PH_ADD(19, clock64() - phS);
+#endif
         // a path that ended at its camera hit (max_bounce 0) leaves its lane idle: hand out again
         if (drained || __ballot(ended) == 0) break;
       }
@@ -548,8 +573,9 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
       PH_ADD(5, __popcll(act));
       phT = clock64();
 #endif
-      walk4Run<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0), FULL>(p.scene, s.o, s.d, s.kind == K_SHADOW, w,
-                                                                           st, top, PT_REGEN_YIELD, ph);
+      walk4Run<CULL, StackT<REGEN_LDS_STACK, BS>, (LDS_NODES > 0), FULL,
+               INTEG == 2 ? PT_LEAF_WAIT_MIS : PT_LEAF_WAIT_U>(p.scene, s.o, s.d, s.kind == K_SHADOW, w, st, top,
+                                                              PT_REGEN_YIELD, ph);
 #if PT_PHASE_STATS
       PH_ADD(1, clock64() - phT);
       if (__ballot(!walk4Done(w)) == 0) PH_ADD(13, 1);
@@ -597,7 +623,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
 #undef PH_ADD
 #if PT_PHASE_STATS
   if (lane == 0) ph[15] = clock64() - phStart;
-  if (p.waveTrace && lane < 16) p.waveTrace[16 * ((size_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6)) + lane] = ph[lane];
+  if (p.waveTrace && lane < PHASE_WORDS)
+    p.waveTrace[PHASE_WORDS * ((size_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6)) + lane] = ph[lane];
 #elif PT_WAVE_TRACE
   if (p.waveTrace && lane == 0) {
     unsigned long long* r = p.waveTrace + 6 * ((size_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6));

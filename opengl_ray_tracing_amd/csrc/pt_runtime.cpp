@@ -284,10 +284,17 @@ const char* pt_last_error(pt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_creat
 //    longest tiles: c4 at N = 1 0.2566 -> 0.2531 ms per frame over 200 frames and 0.3288 -> 0.2860
 //    over 20 from an idle GPU, N = 2 0.139 -> 0.131, N = 4 / 8 equal (profiles/r4/batch_c4/);
 //  * 1 x on large Disney/MIS scenes, whose frames are long already (c5 5.66 ms at 1, 5.86 at 2).
+// With few hardware queues (GPU_MAX_HW_QUEUES 4, HIP's default and the GPU box's: 2 frames in flight)
+// a launch takes more frames, so that about as much work is in flight: Lambert 8 x, Disney/MIS 16 x,
+// large scenes 2 x (round 5, 4 queues, the driver's 20-frame bench window from an idle GPU: c2 at
+// 2 / 4 / 6 / 8 / 12 / 16 frames per launch 0.218 / 0.196 / 0.187 / 0.184 / 0.178 / 0.184 ms per
+// frame; c4 at 4 / 8 / 16 0.342 / 0.302 / 0.271; c5 at 1 / 2 4.59 / 4.34; c2's shares at 20 frames,
+// N = 2 / 4 / 8, at 2 x N 0.116 / 0.066 / 0.041 and 4 x N 0.107 / 0.060 / 0.041 ms).
 static int batchFor(const pt_ctx* ctx, bool wideScene) {
   const pt_config& c = ctx->cfg;
   if (c.frame_batch > 0) return std::min(c.frame_batch, MAX_BATCH);
-  const int m = wideScene ? 1 : c.integrator == 0 ? 2 : 4;
+  const bool fewQueues = ctx->pipeDepth <= 3;
+  const int m = wideScene ? (fewQueues ? 2 : 1) : c.integrator == 0 ? (fewQueues ? 8 : 2) : (fewQueues ? 16 : 4);
   return std::max(1, std::min(m * std::max(1, c.tile_world), MAX_BATCH));
 }
 

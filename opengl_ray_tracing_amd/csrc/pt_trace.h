@@ -14,6 +14,12 @@ struct Counters {
   uint32_t rays, nodes, tris, mats, texels;
 };
 
+// The node phase of a while-while walk (traceRay, traceRay4; walk4Run has PT_LEAF_WAIT) ends once
+// at most this many of its lanes still look for a leaf (0: every lane holds one)
+#ifndef PT_LEAF_WAIT_MK
+#define PT_LEAF_WAIT_MK 0
+#endif
+
 // ----------------------------------------------------------------- stack
 // LDS stack of up to DEPTH entries per lane, entry e of thread t at
 // lds[(e % DEPTH) * STRIDE + t] (lane-interleaved: a wave's push/pop is bank
@@ -332,14 +338,18 @@ __device__ __forceinline__ int traceRay(const SceneView& S, V3 o, V3 d, float& t
         next = st.sp > 0 ? st.pop() : REF_NONE;
       }
       ref = next;
-      if (__ballot(leaf == REF_NONE) == 0) break;  // every lane still walking holds a leaf
+      // every lane still walking holds a leaf (or at most PT_LEAF_WAIT_MK still look for one)
+      if (__popcll(__ballot(leaf == REF_NONE)) <= PT_LEAF_WAIT_MK) break;
     }
     // leaf phase
     if (leaf == REF_NONE && isLeafRef(ref)) {
       leaf = ref;
       ref = st.sp > 0 ? st.pop() : REF_NONE;
     }
-    if (leaf == REF_NONE) break;  // ref == REF_NONE too: done
+    if (leaf == REF_NONE) {
+      if (ref >= 0) continue;  // left the node phase early (PT_LEAF_WAIT_MK): on with its nodes
+      break;                   // ref == REF_NONE too: done
+    }
     {
       uint32_t v = ~(uint32_t)leaf;
       int start = (int)(v >> LEAF_CNT_BITS);
@@ -491,13 +501,16 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
         next = st.sp > 0 ? st.pop() : REF_NONE;
       }
       ref = next;
-      if (__ballot(leaf == REF_NONE) == 0) break;
+      if (__popcll(__ballot(leaf == REF_NONE)) <= PT_LEAF_WAIT_MK) break;
     }
     if (leaf == REF_NONE && isLeafRef(ref)) {
       leaf = ref;
       ref = st.sp > 0 ? st.pop() : REF_NONE;
     }
-    if (leaf == REF_NONE) break;
+    if (leaf == REF_NONE) {
+      if (ref >= 0) continue;  // left the node phase early (PT_LEAF_WAIT_MK): on with its nodes
+      break;
+    }
     const uint32_t v = ~(uint32_t)leaf;
     const int start = (int)(v >> LEAF_CNT_BITS);
     const int cnt = (int)(v & ((1u << LEAF_CNT_BITS) - 1u)) + 1;
@@ -532,10 +545,15 @@ __device__ __forceinline__ int traceRay4(const SceneView& S, V3 o, V3 d, float& 
 }
 
 // ----------------------------------------------------------------- resumable 4-wide walk
-// c2 (100 frames, 4 rounds, profiles/r5/ab): 0 (every lane holds a leaf: the while-while) 0.1843 ms
-// per frame, 4 0.1803
-#ifndef PT_LEAF_WAIT
-#define PT_LEAF_WAIT 4
+// The resumable walk's node phase ends once at most LW of its lanes still look for a leaf (0: every
+// lane holds one, the while-while); the few still looking go on after the leaf phase. Measured
+// (profiles/r5/ab, wall ms per frame): c2 (Lambert) LW 0 / 4 / 8 / 12 / 16: 0.1864 / 0.1807-0.1814 /
+// 0.1795 / 0.1805 / 0.1853; c5 (MIS) 0 / 4 / 8 / 12 / 16: 4.88 / 4.25-4.28 / 4.21 / 4.17 / 4.16
+#ifndef PT_LEAF_WAIT_U
+#define PT_LEAF_WAIT_U 8
+#endif
+#ifndef PT_LEAF_WAIT_MIS
+#define PT_LEAF_WAIT_MIS 12
 #endif
 // traceRay4 as a walk that can stop and resume (the regen kernel's dynamic ray
 // fetch, PT_REGEN_YIELD): the walk's state is a Walk4 plus the lane's stack, and
@@ -565,7 +583,7 @@ __device__ __forceinline__ void walk4Begin(const SceneView& S, Walk4& w, StackTy
   C.rays++;
 }
 // ALL: every node is in LDS at `top`, swizzled (loadNode4Lds); else the first S.f4nTop are, in order
-template <bool CULL, class StackType, bool LDSTOP, bool ALL = false>
+template <bool CULL, class StackType, bool LDSTOP, bool ALL = false, int LW = PT_LEAF_WAIT_U>
 __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool anyRT, Walk4& w, StackType& st,
                                          const float4* top, int yield, unsigned long long* ph = nullptr) {
   const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -627,9 +645,8 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
         next = st.sp > 0 ? st.pop() : REF_NONE;
       }
       w.ref = next;
-      // the node phase ends once at most PT_LEAF_WAIT of its lanes still look for a leaf (0: every
-      // lane holds one, traceRay's while-while); the few still looking go on after the leaf phase
-      if (__popcll(__ballot(w.leaf == REF_NONE)) <= PT_LEAF_WAIT) break;
+      // the node phase ends once at most LW of its lanes still look for a leaf (above)
+      if (__popcll(__ballot(w.leaf == REF_NONE)) <= LW) break;
     }
     if (w.leaf == REF_NONE && isLeafRef(w.ref)) {
       w.leaf = w.ref;

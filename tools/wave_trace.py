@@ -49,8 +49,8 @@ PHASES = ["refill", "walk", "reference check", "shading"]
 
 
 def phases(path):
-    """PT_PHASE_STATS records (pt_regen.hip): 16 u64 per wave, summed over every wave of every frame."""
-    raw = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.float64)
+    """PT_PHASE_STATS records (pt_regen.hip): 24 u64 per wave, summed over every wave of every frame."""
+    raw = np.fromfile(path, dtype=np.uint64).reshape(-1, 24).astype(np.float64)
     raw = raw[raw[:, 15] > 0]
     t = raw.sum(axis=0)
     life = t[15]
@@ -64,6 +64,10 @@ def phases(path):
     print(f"node iterations {t[7]:.3g} ({t[7] / it:.1f} per walk call), lanes {t[8] / max(t[7], 1):5.1f} of 64")
     print(f"pair tests      {t[9]:.3g} ({t[9] / it:.1f} per walk call), lanes {t[10] / max(t[9], 1):5.1f} of 64")
     print(f"refill iterations {t[11]:.3g}; retraced lanes {t[14]:.3g}")
+    if t[17] > 0:  # the uniform integrators' hand-out (TILE_PRIM)
+        print(f"  refill = hand-out {t[16] / life:6.3f} (of it tile claims {t[18] / life:6.3f}: {t[17]:.3g} claims, "
+              f"{t[18] / max(t[17], 1) / 2.4e3:.2f} us each) + camera-hit shading {t[19] / life:6.3f} "
+              f"({t[21]:.3g} passes, {t[20] / max(t[21], 1):.1f} lanes each)")
 
 
 def main():
