@@ -389,8 +389,11 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
     }
     ctx->pipeDepthBase = ctx->pipeDepth;
     ctx->batchCap = batchFor(ctx, false);
-    // slot streams are created as a depth first uses them (ensureSlots): streams beyond the
-    // hardware queues share queues, which serialises their work
+    // slot streams are created as a depth first uses them (ensureSlots). (Created here instead,
+    // before the context's own stream and the caller's, they take hardware queues of their own even
+    // at GPU_MAX_HW_QUEUES = 4 -- created later they share one -- but c2's shares measured slower
+    // that way in the 20-frame window, N = 2 / 4 / 8: 0.1091 / 0.0638 / 0.0439 -> 0.1164 / 0.0701 /
+    // 0.0478 ms: the next launch's camera-ray pass then competes with the running launch's tail.)
     for (int k = 0; k < COLS; k++) CKC(hipEventCreateWithFlags(&ctx->mixDone[k], hipEventDisableTiming));
     CKC(hipEventCreateWithFlags(&ctx->binsBuilt, hipEventDisableTiming));
   }

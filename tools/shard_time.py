@@ -43,7 +43,8 @@ def main():
                       tile_world=n, frame_batch=mul * n if mul else batch) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
-            g = FrameGather(r, 0, n, "cuda:0", mode="accum", proxy=True) if with_gather and n > 1 else None
+            g = FrameGather(r, 0, n, "cuda:0", mode="accum", proxy=True,
+                            overlap=os.environ.get("PT_SHARD_OVERLAP", "1") != "0") if with_gather and n > 1 else None
             per = r.stats().frame_batch
 
             def frames(first, k):  # bench.py's frames(): batches, each followed by the gather
