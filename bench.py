@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--no-psnr", action="store_true", help="skip the spp-matched PSNR check")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="cpu_baseline sample: full frames are rendered until this much CPU wall time has passed")
-    ap.add_argument("--counters", default=str(ROOT / "profiles" / "r4" / "counters.json"),
+    ap.add_argument("--counters", default=str(ROOT / "profiles" / "r5" / "counters.json"),
                     help="per-launch PMC counters of the bench kernel per config (tools/roofline.py)")
     ap.add_argument("--no-reset", action="store_true", help="skip the reset_ms_per_frame frames (profiling runs)")
     ap.add_argument("--no-serial", action="store_true", help="skip the serial-frames run (roofline.kernel_basis)")

@@ -56,7 +56,10 @@ static constexpr int EV_RING = 64;
 #define PT_PIPE 8  // frames in flight (PT_PIPE_DEPTH overrides; capped by the hardware queues)
 #endif
 static constexpr int PIPE = MAX_SLOTS;      // most frames in flight
-static constexpr int MAX_BATCH = 16;        // most frames per launch (pt_render_frames_async)
+#ifndef PT_MAX_BATCH
+#define PT_MAX_BATCH 16
+#endif
+static constexpr int MAX_BATCH = PT_MAX_BATCH;  // most frames per launch (pt_render_frames_async)
 // colour buffers: a launch reuses the buffer of the launch 2 * depth + 1 back, whose running-mean
 // update is then long done -- with depth + 1 the wait made a slot's next frame follow the
 // running-mean update of the previous frame on another slot (two cross-queue hops), and an N = 8
