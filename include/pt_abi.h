@@ -103,7 +103,7 @@ typedef struct pt_config {
   int device_ids[PT_MAX_DEVICES];
   int gather;
   /* ABI 6 */
-  int frame_batch;    /* pt_render_frames_async: most frames per launch, at most 16 (0 = automatic:
+  int frame_batch;    /* pt_render_frames_async: most frames per launch, at most 32 (0 = automatic:
                          2 x tile_world frames with the Lambert integrator, 4 x tile_world with
                          Disney/MIS, tile_world with Disney/MIS on scenes of more than 48 MB of
                          records -- 8 x / 16 x / 2 x when the hardware queues allow at most 3

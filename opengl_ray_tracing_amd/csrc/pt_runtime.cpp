@@ -56,8 +56,10 @@ static constexpr int EV_RING = 64;
 #define PT_PIPE 8  // frames in flight (PT_PIPE_DEPTH overrides; capped by the hardware queues)
 #endif
 static constexpr int PIPE = MAX_SLOTS;      // most frames in flight
+// 32: c2's 1/8 share in the 20-frame bench window at 4 hardware queues 0.0417 -> 0.0351 ms per
+// frame (its 20 frames one launch instead of 16 + 4), 1/4 share 0.0593 -> 0.0569, c4 0.2736 -> 0.2701
 #ifndef PT_MAX_BATCH
-#define PT_MAX_BATCH 16
+#define PT_MAX_BATCH 32
 #endif
 static constexpr int MAX_BATCH = PT_MAX_BATCH;  // most frames per launch (pt_render_frames_async)
 // colour buffers: a launch reuses the buffer of the launch 2 * depth + 1 back, whose running-mean
