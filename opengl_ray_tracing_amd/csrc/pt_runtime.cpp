@@ -165,8 +165,9 @@ struct pt_ctx {
   int primCap[PIPE] = {};                   // frames each slot's camera-ray results hold
   // the large-scene path (regen kernel at 4 waves/SIMD, 4-wide walk with dynamic ray fetch,
   // camera-ray pass) on scenes of any size: -1 = for the Lambert integrator (c2 0.342 ->
-  // 0.251 ms/frame; MIS c4 0.355 -> 0.468, Disney-MIS c3 0.160 -> 0.163: those keep the
-  // megakernel); PT_FLAG_REGEN / PT_FLAG_MEGAKERNEL choose per context
+  // 0.251 ms/frame) and the MIS integrator at 2 bounces (round 5: c3 0.1443 -> 0.1331; c4's 8
+  // bounces keep the megakernel); PT_FLAG_REGEN / PT_FLAG_MEGAKERNEL choose per context,
+  // PT_REGEN_WIDE = 1 / 0 (environment) for every / no scene
   int regenWide = -1;
   hipStream_t slotStream[PIPE] = {};
   hipEvent_t kernelDone[PIPE] = {};         // slot's last frame kernel (+ reorder) ended
@@ -370,6 +371,9 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   ctx->perQueue = (ctx->numItems + NUM_QUEUES - 1) / NUM_QUEUES;
   // the default megakernel and the regen kernel pipeline their frames (not BASIC, the fetch
   // counter or PT_FLAG_SERIAL_FRAMES)
+  // the path-regeneration kernel with the 4-wide walk for every integrator on any scene
+  // (PT_REGEN_WIDE = 1; 0: never; unset: Lambert frames and large Disney/MIS scenes)
+  if (const char* e = std::getenv("PT_REGEN_WIDE")) ctx->regenWide = std::atoi(e) != 0 ? 1 : 0;
   ctx->pipe = cfg->integrator != PT_BASIC_CPU_COMPAT &&
               !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_SERIAL_FRAMES));
   if (ctx->pipe) {
@@ -1477,7 +1481,13 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // leave a lock-step wave's lanes idle
   const size_t sceneBytes = (size_t)ctx->nTri * (PAIR_F4 * 16 + 64 + HIT_F4 * 16) + (size_t)ctx->nDevNodes * 64;
   const bool wideScene = !count && cull && c.integrator != 0 && sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20);
-  const bool regenAll = !count && cull && (ctx->regenWide > 0 || (ctx->regenWide < 0 && c.integrator == 0));
+  // ... and the MIS integrator at its shader's own 2 bounces (IS:861): c3 at 4 hardware queues 0.1443 ->
+  // 0.1331 ms per frame on the regen kernel (round 5); deeper MIS paths keep the megakernel (c4, 8
+  // bounces: 0.270 vs 0.370)
+  const int mbounce = c.max_bounce >= 0 ? c.max_bounce : defaultBounce(c.integrator);
+  const bool regenAll = !count && cull &&
+                        (ctx->regenWide > 0 ||
+                         (ctx->regenWide < 0 && (c.integrator == 0 || (c.integrator == 2 && mbounce <= 2))));
   const bool regen =
       !count && ((c.flags & PT_FLAG_REGEN) || ((wideScene || regenAll) && !(c.flags & PT_FLAG_MEGAKERNEL)));
   // this frame's stream and per-frame buffers: slot frameNo % depth, colour buffer
