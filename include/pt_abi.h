@@ -33,7 +33,7 @@ extern "C" {
                              6: batches of frames (pt_render_frames_async, pt_config.frame_batch,
                                 pt_frame_stats.frames), pt_config.hw_queues;
                              7: pt_unpack_ranks (every other rank's f32 gather in one launch);
-                                PT_FLAG_WAVEFRONT retired */
+                                PT_FLAG_WAVEFRONT retired; pt_frame_stats.env_compact, tree4_nodes */
 
 /* error codes */
 #define PT_OK 0
@@ -145,6 +145,10 @@ typedef struct pt_frame_stats {
   int64_t frames;       /* frames rendered by the launches since the reset (a batch launch renders
                            several: pt_render_frames_async) */
   int frame_batch;      /* most frames per launch of this context (pt_config.frame_batch, resolved) */
+  /* ABI 7 */
+  int env_compact;      /* 1: the env is read from its compact texels (RGBE + pdf, 16-bit sample table),
+                           which decode to the uploaded floats bit for bit; 0: from the float texels */
+  int tree4_nodes;      /* 4-wide runtime-tree nodes (0: none) */
 } pt_frame_stats;
 
 typedef struct pt_ctx pt_ctx;

@@ -42,7 +42,7 @@ class PtFrameStats(C.Structure):
         ("waves_per_simd", C.c_int), ("devices", C.c_int), ("gather", C.c_int), ("frames_in_flight", C.c_int),
         ("upload_ms", C.c_float), ("accel_build_ms", C.c_float), ("accel_device", C.c_int),
         ("accel_nodes", C.c_int), ("accel_depth", C.c_int), ("regen", C.c_int),
-        ("frames", C.c_int64), ("frame_batch", C.c_int),
+        ("frames", C.c_int64), ("frame_batch", C.c_int), ("env_compact", C.c_int), ("tree4_nodes", C.c_int),
     ]
 
 

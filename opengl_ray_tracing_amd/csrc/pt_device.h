@@ -171,14 +171,50 @@ __device__ __forceinline__ void stStream(float4* p, float4 v) {
 #endif
 }
 
-template <class T>
-__device__ __forceinline__ T texNearest(const T* img, int w, int h, float u, float v) {
+// GL_NEAREST + GL_CLAMP_TO_EDGE addressing (OpenglRayTracing/main.cpp:184-194): the texel of (u, v)
+__device__ __forceinline__ int texIndex(int w, int h, float u, float v) {
   float fx = floorf(u * (float)w);
   float fy = floorf(v * (float)h);
   fx = fminf(fmaxf(fx, 0.0f), (float)(w - 1));
   fy = fminf(fmaxf(fy, 0.0f), (float)(h - 1));
   int x = (int)fx, y = (int)fy;
-  return ldStream(img + y * w + x);
+  return y * w + x;
+}
+template <class T>
+__device__ __forceinline__ T texNearest(const T* img, int w, int h, float u, float v) {
+  return ldStream(img + texIndex(w, h, u, v));
+}
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 ldStream(const uint2* p) {
+#if PT_NT_STREAM
+  const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+  return make_uint2(v.x, v.y);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ uint32_t ldStream(const uint32_t* p) {
+#if PT_NT_STREAM
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+// the compact env texels (pt_kernels.h Env): RGBE channels m * 2^(E - 136) -- exact products of an
+// integer below 256 and a power of two -- and the pdf's own bits; the sample table's float(x) / w,
+// float(y) / h with IEEE division, as calculateHdrCache computes them (IS main.cpp:630-631)
+__device__ __forceinline__ float4 decodeHdr8(uint2 t) {
+  const float sc = ldexpf(1.0f, (int)(t.x >> 24) - 136);
+  return make_float4((float)(t.x & 255u) * sc, (float)((t.x >> 8) & 255u) * sc, (float)((t.x >> 16) & 255u) * sc,
+                     __uint_as_float(t.y));
+}
+__device__ __forceinline__ float2 decodeCache4(uint32_t v, int w, int h) {
+  return make_float2((float)(v & 0xffffu) / (float)w, (float)(v >> 16) / (float)h);
+}
+// the env texel (r, g, b, pdf) of (u, v), from the compact or the float4 texels
+__device__ __forceinline__ float4 envTexel(const Env& e, float u, float v) {
+  const int k = texIndex(e.w, e.h, u, v);
+  return e.hdr8 ? decodeHdr8(ldStream(e.hdr8 + k)) : ldStream(e.hdr + k);
 }
 // SampleSphericalMap IS:175-181 / toSphericalCoord IS:638-644
 __device__ __forceinline__ void toSpherical(V3 v, float& u, float& w) {
@@ -195,7 +231,7 @@ __device__ __forceinline__ V3 sampleHdr(const Env& e, V3 v) {
   if (!e.hdr) return v3(0, 0, 0);
   float u, w;
   toSpherical(normalize(v), u, w);
-  float4 c = texNearest(e.hdr, e.w, e.h, u, w);
+  float4 c = envTexel(e, u, w);
   return v3(fminf(c.x, 10.0f), fminf(c.y, 10.0f), fminf(c.z, 10.0f));
 }
 // hdrColor IS:647-651 (unclamped)
@@ -203,13 +239,15 @@ __device__ __forceinline__ V3 hdrColor(const Env& e, V3 L) {
   if (!e.hdr) return v3(0, 0, 0);
   float u, w;
   toSpherical(normalize(L), u, w);
-  float4 c = texNearest(e.hdr, e.w, e.h, u, w);
+  float4 c = envTexel(e, u, w);
   return v3(c.x, c.y, c.z);
 }
 // SampleHdr IS:573-585, in two parts: the cache texel of (xi1, xi2) and the
 // direction it encodes (split so a caller can issue the fetch early)
 __device__ __forceinline__ float2 hdrCacheTexel(const Env& e, float xi1, float xi2) {
-  return e.cache ? texNearest(e.cache, e.w, e.h, xi1, xi2) : make_float2(0.0f, 0.0f);
+  if (!e.cache) return make_float2(0.0f, 0.0f);
+  const int k = texIndex(e.w, e.h, xi1, xi2);
+  return e.cache4 ? decodeCache4(ldStream(e.cache4 + k), e.w, e.h) : ldStream(e.cache + k);
 }
 __device__ __forceinline__ V3 hdrDirFromCache(float2 c) {
   float x = c.x, y = c.y;
@@ -228,7 +266,7 @@ __device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
 __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
   float u, w;
   toSpherical(normalize(L), u, w);
-  float pdf = e.hdr ? texNearest(e.hdr, e.w, e.h, u, w).w : 0.0f;
+  float pdf = e.hdr ? envTexel(e, u, w).w : 0.0f;
   float theta = PT_PI * (0.5f - w);
   float sin_theta = fmaxf(ptm_sinf(theta), 1e-10f);
   float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
@@ -242,7 +280,7 @@ __device__ __forceinline__ float hdrPdf(const Env& e, V3 L) {
 __device__ __forceinline__ float4 hdrTexelOf(const Env& e, V3 L, float& w) {
   float u;
   toSpherical(normalize(L), u, w);
-  return e.hdr ? texNearest(e.hdr, e.w, e.h, u, w) : make_float4(0, 0, 0, 0);
+  return e.hdr ? envTexel(e, u, w) : make_float4(0, 0, 0, 0);
 }
 __device__ __forceinline__ void hdrColorPdfOf(const Env& e, float4 c, float w, V3& color, float& pdf) {
   color = v3(c.x, c.y, c.z);

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pt_device.h"
 #include "pt_kernels.h"
 
 namespace pt {
@@ -129,6 +130,52 @@ __global__ void envPackKernel(float4* hdr, const float4* cache, float2* samp, in
   const float4 c = cache[k];
   hdr[k].w = c.z;
   samp[k] = make_float2(c.x, c.y);
+}
+
+// The compact env texels (pt_kernels.h Env::hdr8 / cache4), each kept only if it decodes to the
+// float texel bit for bit with the decoder the frame kernels use (pt_device.h decodeHdr8 /
+// decodeCache4); *bad is set otherwise (an env not from a Radiance file, or a sample table not
+// from calculateHdrCache) and the float texels stay in use.
+__global__ void envCompactKernel(const float4* hdr, const float2* cache, int w, int h, uint2* hdr8, uint32_t* cache4,
+                                 int n, int* bad) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float4 c = hdr[k];
+  const float mx = fmaxf(c.x, fmaxf(c.y, c.z));
+  bool ok = c.x >= 0.0f && c.y >= 0.0f && c.z >= 0.0f;  // (false for NaN)
+  uint32_t word = 0;
+  if (ok && mx > 0.0f) {
+    int ex;
+    (void)frexpf(mx, &ex);  // mx = f * 2^ex, f in [0.5, 1): the largest channel's m in [128, 256)
+    const int E = ex + 128;
+    ok = E >= 0 && E <= 255;
+    if (ok) {
+      const float inv = ldexpf(1.0f, 136 - E);  // exact scalings by powers of two
+      const float mr = c.x * inv, mg = c.y * inv, mb = c.z * inv;
+      ok = mr == floorf(mr) && mg == floorf(mg) && mb == floorf(mb) && mr <= 255.0f && mg <= 255.0f && mb <= 255.0f;
+      if (ok) word = (uint32_t)mr | (uint32_t)mg << 8 | (uint32_t)mb << 16 | (uint32_t)E << 24;
+    }
+  }
+  const uint2 t = make_uint2(word, __float_as_uint(c.w));
+  const float4 d = decodeHdr8(t);
+  ok = ok && __float_as_uint(d.x) == __float_as_uint(c.x) && __float_as_uint(d.y) == __float_as_uint(c.y) &&
+       __float_as_uint(d.z) == __float_as_uint(c.z);
+  hdr8[k] = t;
+  const float2 q = cache[k];
+  const float fx = rintf(q.x * (float)w), fy = rintf(q.y * (float)h);
+  bool okc = fx >= 0.0f && fx <= 65535.0f && fy >= 0.0f && fy <= 65535.0f;
+  const uint32_t v = okc ? ((uint32_t)fx | (uint32_t)fy << 16) : 0u;
+  const float2 e = decodeCache4(v, w, h);
+  okc = okc && __float_as_uint(e.x) == __float_as_uint(q.x) && __float_as_uint(e.y) == __float_as_uint(q.y);
+  cache4[k] = v;
+  if (!ok || !okc) atomicOr(bad, 1);
+}
+
+hipError_t launchEnvCompact(const float4* hdr, const float2* cache, int w, int h, uint2* hdr8, uint32_t* cache4,
+                            int* bad, hipStream_t s) {
+  const int n = w * h;
+  hipLaunchKernelGGL(envCompactKernel, dim3((n + 255) / 256), dim3(256), 0, s, hdr, cache, w, h, hdr8, cache4, n, bad);
+  return hipGetLastError();
 }
 
 hipError_t launchEnvPack(float4* hdr, const float4* cache, float2* samp, int n, hipStream_t s) {

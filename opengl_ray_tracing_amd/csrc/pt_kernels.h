@@ -162,6 +162,13 @@ struct SceneView {
 struct Env {
   const float4* hdr;    // w x h: (r, g, b, calculateHdrCache pdf) (row 0 = first scanline); null = black
   const float2* cache;  // calculateHdrCache sample table (x, y); null exactly when hdr is null
+  // The same texels in half the bytes, used when non-null (pt_runtime.cpp envOne builds them when
+  // every texel round-trips bit for bit, pt_envcache.hip envCompactKernel): hdr8 = {r | g << 8 |
+  // b << 16 | E << 24, pdf bits}, each channel m * 2^(E - 136) -- the Radiance RGBE form the
+  // reference's decoder expands (hdrloader.cpp:99-104) -- and cache4 = x | y << 16, the sample
+  // table's float(x) / w and float(y) / h (IS main.cpp:630-631)
+  const uint2* hdr8;
+  const uint32_t* cache4;
   int w, h, res;        // res = hdrResolution
 };
 
@@ -327,6 +334,8 @@ hipError_t collapseWide4Device(const BuildNode* nodes, int nNodes, int leafSize,
 // calculateHdrCache on the device (pt_envcache.hip); scratch: 2*w*h + 2*w + 1 floats
 hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* scratch, hipStream_t s);
 // hdr[k].w = cache[k].z, samp[k] = cache[k].xy (the Env render layout)
+hipError_t launchEnvCompact(const float4* hdr, const float2* cache, int w, int h, uint2* hdr8, uint32_t* cache4,
+                            int* bad, hipStream_t s);
 hipError_t launchEnvPack(float4* hdr, const float4* cache, float2* samp, int n, hipStream_t s);
 hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count,
                         bool wide = false);

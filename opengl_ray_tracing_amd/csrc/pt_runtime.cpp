@@ -124,6 +124,8 @@ struct pt_ctx {
   // env
   float4* d_hdr = nullptr;
   float2* d_cache = nullptr;  // sample table (x, y); the pdf lives in d_hdr[k].w
+  uint2* d_hdr8 = nullptr;    // the same texels compacted (pt_kernels.h Env), null = not exact
+  uint32_t* d_cache4 = nullptr;
   int hdrW = 0, hdrH = 0;
   // BASIC shapes, the double image, the replayed random stream
   double* d_shapes = nullptr;
@@ -466,7 +468,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_geo); dfree(ctx->d_hit); dfree(ctx->d_mats); dfree(ctx->d_bvh); dfree(ctx->d_pairs);
   dfree(ctx->d_fbvh); dfree(ctx->d_fbvh4); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri);
   dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
-  dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_shapes);
+  dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_hdr8); dfree(ctx->d_cache4); dfree(ctx->d_shapes);
   dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
@@ -1095,6 +1097,8 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
   CK(hipSetDevice(ctx->cfg.device_id));
   dfree(ctx->d_hdr);
   dfree(ctx->d_cache);
+  dfree(ctx->d_hdr8);
+  dfree(ctx->d_cache4);
   ctx->hdrW = ctx->hdrH = 0;
   if (!hdr) return PT_OK;
   if (w <= 0 || h <= 0) return PT_E_INVALID;
@@ -1121,6 +1125,31 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
     }
     (void)hipFree(full);
     if (rc) return rc;
+  }
+  // The compact texels (8 + 4 bytes instead of 16 + 8 per texel; pt_kernels.h Env), kept when every
+  // texel decodes back to its float bits: a Radiance map's RGBE values and calculateHdrCache's
+  // table always do. c4's MIS light samples read the sample table at uniformly random (xi1, xi2):
+  // half the bytes per texel, twice the texels per cached line. PT_ENV_COMPACT=0: the float texels.
+  static const bool compact = [] {
+    const char* e = std::getenv("PT_ENV_COMPACT");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (compact && w <= 65535 && h <= 65535) {
+    int* d_bad = nullptr;
+    CK(hipMalloc(&ctx->d_hdr8, n * sizeof(uint2)));
+    CK(hipMalloc(&ctx->d_cache4, n * sizeof(uint32_t)));
+    CK(hipMalloc(&d_bad, sizeof(int)));
+    CK(hipMemsetAsync(d_bad, 0, sizeof(int), ctx->stream));
+    hipError_t e = launchEnvCompact(ctx->d_hdr, ctx->d_cache, w, h, ctx->d_hdr8, ctx->d_cache4, d_bad, ctx->stream);
+    int bad = 1;
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("env compact: ") + hipGetErrorString(e));
+    if (bad) {  // not exact: the float texels serve
+      dfree(ctx->d_hdr8);
+      dfree(ctx->d_cache4);
+    }
   }
   ctx->policyKey++;
   ctx->hdrW = w;
@@ -1564,6 +1593,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.scene = sceneView(ctx);
   p.env.hdr = ctx->d_hdr;
   p.env.cache = ctx->d_cache;
+  p.env.hdr8 = ctx->d_hdr8;
+  p.env.cache4 = ctx->d_cache4;
   p.env.w = ctx->hdrW;
   p.env.h = ctx->hdrH;
   p.env.res = ctx->hdrW;
@@ -2130,6 +2161,8 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->launches = ctx->launches;
   st->frames = ctx->frames;
   st->frame_batch = ctx->batchCap;
+  st->env_compact = ctx->d_hdr8 ? 1 : 0;
+  st->tree4_nodes = ctx->fast4Ready ? ctx->f4nDev : 0;
   st->max_stack = ctx->maxStack;
   st->split_items = 0;
   st->runtime_tree = ctx->lastFast ? 1 : 0;

@@ -65,6 +65,8 @@ class FrameStats:
     regen: int = 0
     frames: int = 0       # frames rendered (a batch launch renders several)
     frame_batch: int = 1  # most frames per launch
+    env_compact: int = 0  # the env read from its compact (RGBE) texels
+    tree4_nodes: int = 0  # 4-wide runtime-tree nodes
 
 
 def _fp(a: np.ndarray):
@@ -307,7 +309,7 @@ class Renderer:
                           s.kernel_ms_total, s.launches, s.max_stack, s.split_items, s.runtime_tree,
                           s.waves_per_simd, s.devices, s.gather, s.frames_in_flight, s.upload_ms,
                           s.accel_build_ms, s.accel_device, s.accel_nodes, s.accel_depth, s.regen, s.frames,
-                          s.frame_batch)
+                          s.frame_batch, s.env_compact, s.tree4_nodes)
 
     def reset_stats(self):
         self._ck(self._lib.pt_reset_stats(self._h), "pt_reset_stats")
