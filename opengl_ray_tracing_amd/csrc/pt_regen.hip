@@ -423,7 +423,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
             // (a claim -- the device-scope atomic, then the tile's camera-ray results -- is 1.6-2.3 us
             // and 10-13 % of a c2 wave's time, PT_PHASE_STATS; measured slower: claiming the wave's
             // next tile ahead, c2 0.1807 -> 0.1841 ms, c5 4.25 -> 4.29; 2 / 4 consecutive items per
-            // atomic, c2 0.2106 -> 0.2160 / 0.2390 at 4 hardware queues)
+            // atomic, c2 0.2106 -> 0.2160 / 0.2390 at 4 hardware queues; claiming once the tile has
+            // 8 / 16 / 32 slots left, c2 0.1783 -> 0.1786 / 0.1792 / 0.1793)
             const int item = cur.next(p.queue, p.perQueue, p.numItems, home, tileFr, p.nFrames);
             if (item < 0) {
               drained = true;
