@@ -171,6 +171,7 @@ struct pt_ctx {
   // bounces keep the megakernel); PT_FLAG_REGEN / PT_FLAG_MEGAKERNEL choose per context,
   // PT_REGEN_WIDE = 1 / 0 (environment) for every / no scene
   int regenWide = -1;
+  bool solo = true;                         // PT_SOLO = 0 (environment): every pipelined launch on a slot stream
   hipStream_t slotStream[PIPE] = {};
   hipEvent_t kernelDone[PIPE] = {};         // slot's last frame kernel (+ reorder) ended
   bool slotBusy[PIPE] = {};                 // kernelDone[k] has been recorded since the last sync
@@ -376,6 +377,7 @@ static int createOne(pt_ctx** out, const pt_config* cfg) {
   // the path-regeneration kernel with the 4-wide walk for every integrator on any scene
   // (PT_REGEN_WIDE = 1; 0: never; unset: Lambert frames and large Disney/MIS scenes)
   if (const char* e = std::getenv("PT_REGEN_WIDE")) ctx->regenWide = std::atoi(e) != 0 ? 1 : 0;
+  if (const char* e = std::getenv("PT_SOLO")) ctx->solo = std::atoi(e) != 0;
   ctx->pipe = cfg->integrator != PT_BASIC_CPU_COMPAT &&
               !(cfg->flags & (PT_FLAG_COUNT_FETCHES | PT_FLAG_SERIAL_FRAMES));
   if (ctx->pipe) {
@@ -1529,7 +1531,17 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const int slot = piped ? (int)(ctx->frameNo % (unsigned)D) : 0;
   const int nCol = 2 * D + 1;
   const int colIdx = piped ? (int)(ctx->frameNo % (unsigned)nCol) : 0;
-  hipStream_t S = piped ? ctx->slotStream[slot] : ctx->stream;
+  // A launch issued while no other is in flight runs on the caller's stream itself: its camera-ray
+  // pass, frame kernel and running-mean update -- and the caller's next work (the gather's pack) --
+  // then follow one another in one queue instead of across queues (an event wait between hardware
+  // queues costs ~15-18 us per hop; c2's 1/8 share of a 20-frame window is one launch)
+  bool solo = piped && ctx->solo;
+  if (solo) {
+    for (int k = 0; k < D; k++)
+      if (ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady) solo = false;
+    (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
+  }
+  hipStream_t S = piped && !solo ? ctx->slotStream[slot] : ctx->stream;
   // every other slot's frame in flight has ended on S (the frames that read buffers
   // rebuilt below)
   auto waitOthers = [&]() -> int {
@@ -1586,7 +1598,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const size_t npix = (size_t)c.width * c.height;
   // the colour buffer's previous launch (nCol back) has been mixed (the slot's queue counters,
   // order list and camera-ray results belong to its previous launch on this same stream)
-  if (piped && ctx->frameNo >= (unsigned long long)nCol) CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
+  if (piped && ctx->frameNo >= (unsigned long long)nCol && !(S == ctx->stream && ctx->lastMixStream == S))
+    CK(hipStreamWaitEvent(S, ctx->mixDone[colIdx], 0));
   int* queue = reinterpret_cast<int*>(ctx->d_ctl + CTL_QUEUES) + (size_t)slot * NUM_QUEUES * CTL_LINE_INTS;
   RenderParams p;
   std::memset(&p, 0, sizeof(p));
@@ -1664,6 +1677,16 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // colour buffers instead of ~19 GB)
   const size_t shareN = (size_t)ctx->numItems * 64;
   p.colStride = shareN;
+  // every colour buffer (and below, every slot's camera-ray results) allocated at the first launch that
+  // uses any, so no later launch -- a timed one -- waits for an allocation (c2's 1/8 share: a 19 us
+  // hipMalloc before the sixth launch's first kernel)
+  if (piped)
+    for (int k = 0; k < nCol; k++)
+      if (!ctx->d_col[k]) {
+        const int cap = std::max(nF, ctx->batchCap);
+        CK(hipMalloc(&ctx->d_col[k], (size_t)cap * shareN * sizeof(float4)));
+        ctx->colCap[k] = cap;
+      }
   if (piped && ctx->colCap[colIdx] < nF) {  // room for the launch's frames (each buffer grows once, to batchCap)
     if (ctx->d_col[colIdx]) {
       CK(hipEventSynchronize(ctx->mixDone[colIdx]));  // its last frames' running-mean update has read it
@@ -1712,6 +1735,13 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     p.binTilesX = ctx->bins.tilesX;
     p.binTilesY = ctx->bins.tilesY;
     if (pass) {
+      if (piped)
+        for (int k = 0; k < D; k++)
+          if (!ctx->d_prim[k]) {
+            const int cap = std::max(nF, ctx->batchCap);
+            CK(hipMalloc(&ctx->d_prim[k], (size_t)cap * shareN * sizeof(int2)));
+            ctx->primCap[k] = cap;
+          }
       if (ctx->primCap[slot] < nF) {  // the slot's previous launch (on S) may still read the old results
         if (ctx->d_prim[slot]) {
           CK(hipStreamSynchronize(S));
@@ -1781,7 +1811,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     // the running-mean updates on the caller's stream, in frame order, after this launch's kernel
     CK(hipEventRecord(ctx->kernelDone[slot], S));
     ctx->slotBusy[slot] = true;
-    CK(hipStreamWaitEvent(ctx->stream, ctx->kernelDone[slot], 0));
+    if (S != ctx->slotStream[slot])  // the slot's resources: its stream's later work follows this launch
+      CK(hipStreamWaitEvent(ctx->slotStream[slot], ctx->kernelDone[slot], 0));
+    if (S != ctx->stream) CK(hipStreamWaitEvent(ctx->stream, ctx->kernelDone[slot], 0));
     if (ctx->mixPending && ctx->lastMixStream != ctx->stream)  // the caller switched streams: keep frame order
       CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastCol], 0));
     ctx->lastMixStream = ctx->stream;

@@ -713,7 +713,29 @@ __device__ __forceinline__ bool refReachable(const SceneView& S, int tri, V3 o, 
   if (P.x - lo.x > mu && hi.x - P.x > mu && P.y - lo.y > mu && hi.y - P.y > mu && P.z - lo.z > mu &&
       hi.z - P.z > mu)
     return true;
+  // A leaf box flat in one axis a (a floor or a light quad: lo.a == hi.a bitwise) never passes the
+  // margin test above. Every box on its path brackets the flat plane in a (the boxes nest), so each
+  // box's a-slab values (lo.a - o.a) * inv.a and (hi.a - o.a) * inv.a bracket the plane's own value
+  // ta exactly -- IEEE subtraction and multiplication by one reciprocal are monotone -- and the leaf's
+  // a-slab is [ta, ta]. The path therefore passes when ta > 0 and the ray meets the plane inside the
+  // other two axes' ranges by the margin: their slabs then hold ta with room to spare in every box.
   const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const bool flx = lo.x == hi.x, fly = lo.y == hi.y, flz = lo.z == hi.z;
+  if ((int)flx + (int)fly + (int)flz == 1) {
+    const float ta = flx ? (lo.x - o.x) * inv.x : fly ? (lo.y - o.y) * inv.y : (lo.z - o.z) * inv.z;
+    if (ta > 0.0f && ta < PT_INF) {  // finite (a NaN fails too)
+      const V3 Q = o + d * ta;
+      const float sq = fmaxf(fmaxf(fabsf(Q.x), fmaxf(fabsf(Q.y), fabsf(Q.z))),
+                             fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)))) +
+                       fmaxf(fmaxf(fmaxf(fabsf(lo.x), fabsf(hi.x)), fmaxf(fabsf(lo.y), fabsf(hi.y))),
+                             fmaxf(fabsf(lo.z), fabsf(hi.z))) +
+                       ta + 1.0f;
+      const float mq = 6.103515625e-05f * sq;
+      if ((flx || (Q.x - lo.x > mq && hi.x - Q.x > mq)) && (fly || (Q.y - lo.y > mq && hi.y - Q.y > mq)) &&
+          (flz || (Q.z - lo.z > mq && hi.z - Q.z > mq)))
+        return true;
+    }
+  }
   for (int c = leaf; c != 1; c = S.refParent[c]) {
     if (c <= 0) return false;
     float t0;
