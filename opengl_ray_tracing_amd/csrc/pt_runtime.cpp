@@ -187,11 +187,11 @@ struct pt_ctx {
   int lastCol = -1;                         // colour buffer of the last pipelined frame
   bool mixPending = false;                  // a pipelined frame's update may still be running
   unsigned long long frameNo = 0;           // pipelined frames issued
-  int probeN[4] = {0, 0, 0, 0};        // timed frames: runtime tree, uploaded tree (both unsplit), split, unordered
+  int probeN[4] = {0, 0, 0, 0};        // timed frames: runtime tree, uploaded tree (both unsplit), split
   double probeMs[4] = {0.0, 0.0, 0.0, 0.0};
   long long probeLast[4] = {-1, -1, -1, -1};  // launch number of each slot's last timed frame
   int probeGen = 0;
-  int treeDecided = -1, splitDecided = -1, orderDecided = -1;  // -1 probing, 0 off, 1 on
+  int treeDecided = -1, splitDecided = -1;  // -1 probing, 0 off, 1 on
   unsigned policyKey = 0, probedKey = ~0u;  // bumped by every scene / env upload; the key the decisions were made for
   int orderCap = 0;        // work items per band in d_order
   bool orderValid[PIPE] = {};
@@ -1368,29 +1368,27 @@ static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDep
 //    spare (the MIS integrator, latency-bound) and costs when they do not (the
 //    Lambert megakernel is VALU-bound: a split item's idle lanes still take
 //    issue cycles);
-//  * longest-first tile order itself (per-tile cost atomics, the order lookup
-//    of every claim, the reorder kernel) pays off when tiles differ widely in
-//    cost (c4: 8-bounce MIS around the teapot, 0.59 -> 0.47 ms) and costs when
-//    they do not (c2: 0.347 ms in band order vs 0.372 ordered).
+// (Longest-first tile order -- per-tile cost atomics, the order lookup of every
+// claim, the reorder kernel -- was probed as well until round 5: it cost on the
+// Lambert megakernel, c2 0.347 ms in band order vs 0.372, but Lambert frames run
+// on the regen kernel now, and for the integrators left on the megakernel it
+// never lost: c4 at N = 1 0.268 vs 0.267 ms, c4's 1/8 share in a 20-frame batch
+// 0.072 vs 0.088, while the probe's noisy single-frame choice gave 0.069-0.087.)
 // After a restart of the running mean (frameCounter 0, as on every camera move
 // in the reference): frames 1-2 run the runtime's tree and 3-4 the uploaded
 // one, unsplit; frame 5 runs the runtime's tree while the host, at frame 6,
 // waits for frame 4 (frame 5 is already queued, so the GPU never drains) and
 // keeps the faster tree; frames 6-10 split (the per-tile split state
 // converges), 11-12 are timed, and at frame 14 -- waiting for frame 12 with 13
-// queued -- the faster split policy is kept; frames 15-16 run in band order
-// (no cost recording, no reorder) and at frame 19, waiting for frame 16, the
-// order is kept only if it was faster. No frame waits for its own predecessor. The decisions are kept across later restarts until the scene or
+// queued -- the faster split policy is kept. No frame waits for its own
+// predecessor. The decisions are kept across later restarts until the scene or
 // the env is uploaded again (a camera move changes neither tree's merit nor,
 // measurably, the split policy's), so only the first restart after an upload
 // pays for the probe's slower trial frames; every restart still clears the
-// per-tile split state and cost estimates. Sets *useFast and *noOrder (this
-// frame in band order); returns the split percentage for this frame's reorder
-// (0 = off).
-static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast,
-                       bool* noOrder) {
+// per-tile split state and cost estimates. Sets *useFast; returns the split
+// percentage for this frame's reorder (0 = off).
+static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast) {
   *useFast = fastAllowed;
-  *noOrder = false;
   ctx->tagSlot = -1;
   if (!ordered) return 0;
   if (!PT_SPLIT_AUTO) return PT_SPLIT_PCT;
@@ -1402,9 +1400,8 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
       ctx->probeMs[k] = 0.0;
       ctx->probeLast[k] = -1;
     }
-    const bool keep = ctx->treeDecided >= 0 && ctx->splitDecided >= 0 && ctx->orderDecided >= 0 &&
-                      ctx->probedKey == ctx->policyKey;
-    if (!keep) ctx->treeDecided = ctx->splitDecided = ctx->orderDecided = -1;
+    const bool keep = ctx->treeDecided >= 0 && ctx->splitDecided >= 0 && ctx->probedKey == ctx->policyKey;
+    if (!keep) ctx->treeDecided = ctx->splitDecided = -1;
     ctx->probedKey = ctx->policyKey;
     // split state and cost estimates start over (the camera or scene changed), in
     // every slot's stream order (after its last reorder, before its next frame)
@@ -1422,15 +1419,6 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
   if (f == 14 && ctx->splitDecided < 0) {
     foldUpTo(ctx, ctx->probeLast[2]);
     ctx->splitDecided = PT_SPLIT_PCT > 0 && avg(2) < avg(ctx->treeDecided ? 0 : 1) ? 1 : 0;
-  }
-  if (f == 19 && ctx->orderDecided < 0) {
-    foldUpTo(ctx, ctx->probeLast[3]);
-    ctx->orderDecided = avg(3) < avg(ctx->splitDecided ? 2 : ctx->treeDecided ? 0 : 1) ? 0 : 1;
-  }
-  // this frame's tile order
-  if (ctx->orderDecided == 0 || (ctx->orderDecided < 0 && (f == 15 || f == 16))) {
-    *noOrder = true;
-    if (ctx->orderDecided < 0) ctx->tagSlot = 3;
   }
   // this frame's tree, and the probe slot its time goes to
   if (ctx->treeDecided >= 0) {
@@ -1654,10 +1642,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   int* order = ordered ? ctx->d_order + (size_t)slot * orderInts : nullptr;
   // the tree (the runtime's own, checked against the uploaded one, unless asked
   // not to) and the split policy: probePolicy
-  bool useFast = false, noOrder = false;
+  bool useFast = false;
   const int splitPct = probePolicy(ctx, frameCounter, ordered,
-                                   !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast,
-                                   &noOrder);
+                                   !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast);
   // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
   if (regen && walk4) useFast = true;
   if (regen && wide)  // its own LDS copy's size: the top of the tree, or all of it
@@ -1667,7 +1654,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // While the policy probe times frames (PT_SPLIT_AUTO, 20 frames after a restart) a pipelined
   // frame starts only after the previous one has ended, and each launch is one frame.
   const bool probing = ordered && PT_SPLIT_AUTO &&
-                       (ctx->treeDecided < 0 || ctx->splitDecided < 0 || ctx->orderDecided < 0);
+                       (ctx->treeDecided < 0 || ctx->splitDecided < 0);
   const int nF = piped && !probing ? std::max(1, std::min(want, ctx->batchCap)) : 1;
   if (done) *done = nF;
   p.nFrames = nF;
@@ -1756,11 +1743,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   }
   // a frame in band order (probePolicy) records no costs and launches no reorder; the
   // slot's last order list stays valid for its next ordered frame (any list covers every tile)
-  const bool orderedNow = ordered && !noOrder;
-  p.tileOrder = orderedNow && ctx->orderValid[slot] ? order : nullptr;
+  p.tileOrder = ordered && ctx->orderValid[slot] ? order : nullptr;
   p.orderCap = orderCap;
-  p.tileCost = orderedNow ? cost : nullptr;
-  p.tileCostMax = orderedNow ? cost + ctx->numItems : nullptr;
+  p.tileCost = ordered ? cost : nullptr;
+  p.tileCostMax = ordered ? cost + ctx->numItems : nullptr;
   if (piped && probing) {
     if (int e = waitOthers()) return e;
   }
@@ -1799,7 +1785,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     }
   }
 #endif
-  if (orderedNow) {
+  if (ordered) {
     CK(launchReorder(cost, cost + ctx->numItems, cost + 2 * (size_t)ctx->numItems, cost + 3 * (size_t)ctx->numItems,
                      order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, S));
     ctx->orderValid[slot] = true;

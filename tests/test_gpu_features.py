@@ -501,8 +501,7 @@ def test_camera_restart_keeps_policies_and_restarts_the_mean(name):
 
 @pytest.mark.parametrize("name", ["c2", "c4"])
 def test_band_order_frames_equal_ordered_frames(name):
-    """Frames handed out in band order (PT_FLAG_NO_TILE_ORDER, and the probe's band-order trial
-    frames 15-16 of pt_runtime.cpp probePolicy) give the longest-first frames' image bit for bit,
+    """Frames handed out in band order (PT_FLAG_NO_TILE_ORDER) give the longest-first frames' image bit for bit,
     across the probe and a camera restart (the megakernel's tile hand-out: FLAG_MEGAKERNEL, as
     Lambert frames default to the regen kernel)."""
     from opengl_ray_tracing_amd import FLAG_MEGAKERNEL, FLAG_NO_TILE_ORDER
