@@ -214,7 +214,8 @@ __device__ __forceinline__ float2 decodeCache4(uint32_t v, int w, int h) {
 // the env texel (r, g, b, pdf) of (u, v), from the compact or the float4 texels
 __device__ __forceinline__ float4 envTexel(const Env& e, float u, float v) {
   const int k = texIndex(e.w, e.h, u, v);
-  return e.hdr8 ? decodeHdr8(ldStream(e.hdr8 + k)) : ldStream(e.hdr + k);
+  if (e.nt) return e.hdr8 ? decodeHdr8(ldStream(e.hdr8 + k)) : ldStream(e.hdr + k);
+  return e.hdr8 ? decodeHdr8(e.hdr8[k]) : e.hdr[k];
 }
 // SampleSphericalMap IS:175-181 / toSphericalCoord IS:638-644
 __device__ __forceinline__ void toSpherical(V3 v, float& u, float& w) {
@@ -247,7 +248,8 @@ __device__ __forceinline__ V3 hdrColor(const Env& e, V3 L) {
 __device__ __forceinline__ float2 hdrCacheTexel(const Env& e, float xi1, float xi2) {
   if (!e.cache) return make_float2(0.0f, 0.0f);
   const int k = texIndex(e.w, e.h, xi1, xi2);
-  return e.cache4 ? decodeCache4(ldStream(e.cache4 + k), e.w, e.h) : ldStream(e.cache + k);
+  if (e.nt) return e.cache4 ? decodeCache4(ldStream(e.cache4 + k), e.w, e.h) : ldStream(e.cache + k);
+  return e.cache4 ? decodeCache4(e.cache4[k], e.w, e.h) : e.cache[k];
 }
 __device__ __forceinline__ V3 hdrDirFromCache(float2 c) {
   float x = c.x, y = c.y;

@@ -1599,6 +1599,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.env.w = ctx->hdrW;
   p.env.h = ctx->hdrH;
   p.env.res = ctx->hdrW;
+  p.env.nt = sceneBytes > ((size_t)PT_WIDE_SCENE_MB << 20) ? 1 : 0;
   p.width = c.width;
   p.height = c.height;
   p.frameCounter = frameCounter;
