@@ -147,7 +147,9 @@ typedef struct pt_frame_stats {
   int frame_batch;      /* most frames per launch of this context (pt_config.frame_batch, resolved) */
   /* ABI 7 */
   int env_compact;      /* 1: the env is read from its compact texels (RGBE + pdf, 16-bit sample table),
-                           which decode to the uploaded floats bit for bit; 0: from the float texels */
+                           which decode to the uploaded floats bit for bit; 2: and the sample table by
+                           rows (a row record plus the distinct rows, equal entry by entry); 0: from
+                           the float texels */
   int tree4_nodes;      /* 4-wide runtime-tree nodes (0: none) */
 } pt_frame_stats;
 

@@ -163,6 +163,9 @@ __device__ __forceinline__ float2 ldStream(const float2* p) {
 #endif
 }
 __device__ __forceinline__ void stStream(float4* p, float4 v) {
+#if PT_DIAG_NO_STORE  // diagnostics build (traffic attribution): colours almost never stored
+  if (v.x != -1234.5f) return;
+#endif
 #if PT_NT_STREAM
   const f32x4_t x = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(x, reinterpret_cast<f32x4_t*>(p));
@@ -172,12 +175,17 @@ __device__ __forceinline__ void stStream(float4* p, float4 v) {
 }
 
 // GL_NEAREST + GL_CLAMP_TO_EDGE addressing (OpenglRayTracing/main.cpp:184-194): the texel of (u, v)
-__device__ __forceinline__ int texIndex(int w, int h, float u, float v) {
+__device__ __forceinline__ void texXY(int w, int h, float u, float v, int& x, int& y) {
   float fx = floorf(u * (float)w);
   float fy = floorf(v * (float)h);
   fx = fminf(fmaxf(fx, 0.0f), (float)(w - 1));
   fy = fminf(fmaxf(fy, 0.0f), (float)(h - 1));
-  int x = (int)fx, y = (int)fy;
+  x = (int)fx;
+  y = (int)fy;
+}
+__device__ __forceinline__ int texIndex(int w, int h, float u, float v) {
+  int x, y;
+  texXY(w, h, u, v, x, y);
   return y * w + x;
 }
 template <class T>
@@ -212,8 +220,13 @@ __device__ __forceinline__ float2 decodeCache4(uint32_t v, int w, int h) {
   return make_float2((float)(v & 0xffffu) / (float)w, (float)(v >> 16) / (float)h);
 }
 // the env texel (r, g, b, pdf) of (u, v), from the compact or the float4 texels
+// PT_DIAG_ENV_SMALL (diagnostics builds, traffic attribution): bit 0 keeps every env texel read, bit 1
+// every sample-table read, within the first 1024 texels
+#ifndef PT_DIAG_ENV_SMALL
+#define PT_DIAG_ENV_SMALL 0
+#endif
 __device__ __forceinline__ float4 envTexel(const Env& e, float u, float v) {
-  const int k = texIndex(e.w, e.h, u, v);
+  const int k = texIndex(e.w, e.h, u, v) & ((PT_DIAG_ENV_SMALL & 1) ? 1023 : -1);
   if (e.nt) return e.hdr8 ? decodeHdr8(ldStream(e.hdr8 + k)) : ldStream(e.hdr + k);
   return e.hdr8 ? decodeHdr8(e.hdr8[k]) : e.hdr[k];
 }
@@ -247,7 +260,14 @@ __device__ __forceinline__ V3 hdrColor(const Env& e, V3 L) {
 // direction it encodes (split so a caller can issue the fetch early)
 __device__ __forceinline__ float2 hdrCacheTexel(const Env& e, float xi1, float xi2) {
   if (!e.cache) return make_float2(0.0f, 0.0f);
-  const int k = texIndex(e.w, e.h, xi1, xi2);
+  if (e.cacheRow) {  // the row form (Env::cacheRow): the same entry, as decodeCache4 decodes it
+    int col, row;
+    texXY(e.w, e.h, xi1, xi2, col, row);
+    const uint32_t r = e.cacheRow[row];
+    const uint32_t y = e.cacheY[(size_t)(r >> 16) * e.w + (col & ((PT_DIAG_ENV_SMALL & 2) ? 1023 : -1))];
+    return decodeCache4((r & 0xffffu) | y << 16, e.w, e.h);
+  }
+  const int k = texIndex(e.w, e.h, xi1, xi2) & ((PT_DIAG_ENV_SMALL & 2) ? 1023 : -1);
   if (e.nt) return e.cache4 ? decodeCache4(ldStream(e.cache4 + k), e.w, e.h) : ldStream(e.cache + k);
   return e.cache4 ? decodeCache4(e.cache4[k], e.w, e.h) : e.cache[k];
 }

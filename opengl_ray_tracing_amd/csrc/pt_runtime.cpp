@@ -126,6 +126,8 @@ struct pt_ctx {
   float2* d_cache = nullptr;  // sample table (x, y); the pdf lives in d_hdr[k].w
   uint2* d_hdr8 = nullptr;    // the same texels compacted (pt_kernels.h Env), null = not exact
   uint32_t* d_cache4 = nullptr;
+  uint32_t* d_cacheRow = nullptr;           // the sample table by rows (pt_kernels.h Env::cacheRow)
+  unsigned short* d_cacheY = nullptr;
   int hdrW = 0, hdrH = 0;
   // BASIC shapes, the double image, the replayed random stream
   double* d_shapes = nullptr;
@@ -471,6 +473,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_fbvh); dfree(ctx->d_fbvh4); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri);
   dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_hdr8); dfree(ctx->d_cache4); dfree(ctx->d_shapes);
+  dfree(ctx->d_cacheRow); dfree(ctx->d_cacheY);
   dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
@@ -1101,6 +1104,8 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
   dfree(ctx->d_cache);
   dfree(ctx->d_hdr8);
   dfree(ctx->d_cache4);
+  dfree(ctx->d_cacheRow);
+  dfree(ctx->d_cacheY);
   ctx->hdrW = ctx->hdrH = 0;
   if (!hdr) return PT_OK;
   if (w <= 0 || h <= 0) return PT_E_INVALID;
@@ -1151,6 +1156,34 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
     if (bad) {  // not exact: the float texels serve
       dfree(ctx->d_hdr8);
       dfree(ctx->d_cache4);
+    }
+  }
+  if (ctx->d_cache4) {
+    // the sample table by rows (pt_kernels.h Env::cacheRow), kept when every entry of every row equals
+    // its row form: each row's x is one value, and the rows of one x hold the same y's
+    std::vector<uint32_t> c4(n);
+    CK(hipMemcpy(c4.data(), ctx->d_cache4, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> rows(h);
+    std::vector<unsigned short> ys;
+    std::vector<int> idOf(65536, -1);
+    bool ok = true;
+    for (int i = 0; i < h && ok; i++) {
+      const uint32_t* row = c4.data() + (size_t)i * w;
+      const uint32_t x = row[0] & 0xffffu;
+      int id = idOf[x];
+      if (id < 0) {
+        id = idOf[x] = (int)(ys.size() / (size_t)w);
+        for (int j = 0; j < w; j++) ys.push_back((unsigned short)(row[j] >> 16));
+      }
+      const unsigned short* yr = ys.data() + (size_t)id * w;
+      for (int j = 0; j < w && ok; j++) ok = (row[j] & 0xffffu) == x && (row[j] >> 16) == yr[j];
+      rows[i] = x | (uint32_t)id << 16;
+    }
+    if (ok) {
+      CK(hipMalloc(&ctx->d_cacheRow, rows.size() * sizeof(uint32_t)));
+      CK(hipMalloc(&ctx->d_cacheY, ys.size() * sizeof(unsigned short)));
+      CK(hipMemcpy(ctx->d_cacheRow, rows.data(), rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+      CK(hipMemcpy(ctx->d_cacheY, ys.data(), ys.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
     }
   }
   ctx->policyKey++;
@@ -1596,6 +1629,16 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   p.env.cache = ctx->d_cache;
   p.env.hdr8 = ctx->d_hdr8;
   p.env.cache4 = ctx->d_cache4;
+  // the table by rows for the megakernel's frames when the table outgrows an XCD's L2 share: c4's
+  // frame kernel 216 -> 147 MB DRAM-side per frame, time unchanged (0.2914 / 0.2927 ms); its extra
+  // dependent load costs the regen kernels more than their misses (c5 4.20 -> 4.31 ms, c3 0.1083 -> 0.111)
+#ifndef PT_ROW_TABLE
+#define PT_ROW_TABLE 1  // 0: never, 1: the megakernel's frames, 2: every frame (when the table outgrows 4 MB)
+#endif
+  const bool rowTable = PT_ROW_TABLE > 0 && (PT_ROW_TABLE == 2 || !regen) &&
+                        (size_t)ctx->hdrW * ctx->hdrH * sizeof(uint32_t) > ((size_t)4 << 20);
+  p.env.cacheRow = rowTable ? ctx->d_cacheRow : nullptr;
+  p.env.cacheY = rowTable ? ctx->d_cacheY : nullptr;
   p.env.w = ctx->hdrW;
   p.env.h = ctx->hdrH;
   p.env.res = ctx->hdrW;
@@ -2180,7 +2223,7 @@ static int statsOne(pt_ctx* ctx, pt_frame_stats* st) {
   st->launches = ctx->launches;
   st->frames = ctx->frames;
   st->frame_batch = ctx->batchCap;
-  st->env_compact = ctx->d_hdr8 ? 1 : 0;
+  st->env_compact = ctx->d_hdr8 ? (ctx->d_cacheRow ? 2 : 1) : 0;
   st->tree4_nodes = ctx->fast4Ready ? ctx->f4nDev : 0;
   st->max_stack = ctx->maxStack;
   st->split_items = 0;

@@ -65,7 +65,7 @@ class FrameStats:
     regen: int = 0
     frames: int = 0       # frames rendered (a batch launch renders several)
     frame_batch: int = 1  # most frames per launch
-    env_compact: int = 0  # the env read from its compact (RGBE) texels
+    env_compact: int = 0  # the env read from its compact (RGBE) texels (2: and the sample table by rows)
     tree4_nodes: int = 0  # 4-wide runtime-tree nodes
 
 

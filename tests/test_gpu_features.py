@@ -529,18 +529,22 @@ def test_band_order_frames_equal_ordered_frames(name):
 def test_compact_env_texels_for_radiance_maps_only():
     """A Radiance map's texels (RGBE values) and calculateHdrCache's table (float(x) / w) are read
     from their compact form (8 + 4 bytes per texel instead of 16 + 8), which decodes to the uploaded
-    floats bit for bit (the parity tests render with it); an env that does not round-trip -- the
-    synthetic sky of the smoke test -- keeps the float texels, and both give the oracle's image."""
-    cfg, tris, nodes, hdr = scenes.build_config("c2")
+    floats bit for bit, and the table by rows (env_compact 2: a row record and the distinct rows'
+    2-byte y's, pt_kernels.h Env::cacheRow; the megakernel's MIS light samples read it, here the
+    4-bounce frames); an env that does not
+    round-trip -- the synthetic sky of the smoke test -- keeps the float texels, and all give the
+    oracle's image (the parity tests render with the compact forms too)."""
+    cfg, tris, nodes, hdr = scenes.build_config("c4")  # san_giuseppe: the megakernel reads its table by rows
     eye, rot = orbit_camera(*cfg.camera)
     w, h = 96, 54
-    for name, env in [("radiance", hdr), ("synthetic", scenes.synthetic_env(128, 64))]:
-        with Renderer(w, h, "lambert") as r:
-            r.upload_scene(tris, nodes)
-            r.upload_env(env)
-            r.render_frame(eye, rot, 0)
-            st = r.stats()
-            assert st.env_compact == (1 if name == "radiance" else 0), name
-            g = r.accum()
-        o, _ = oracle.Oracle(tris, nodes, env).render(w, h, "lambert", 0, eye, rot)
-        parity.assert_parity(g.reshape(-1, 4), o.reshape(-1, 4), f"env/{name}")
+    for integ, mb in (("lambert", 2), ("mis", 2), ("mis", 4)):
+        for name, env in [("radiance", hdr), ("synthetic", scenes.synthetic_env(128, 64))]:
+            with Renderer(w, h, integ, max_bounce=mb) as r:
+                r.upload_scene(tris, nodes)
+                r.upload_env(env)
+                r.render_frame(eye, rot, 0)
+                st = r.stats()
+                assert st.env_compact == (2 if name == "radiance" else 0), name
+                g = r.accum()
+            o, _ = oracle.Oracle(tris, nodes, env).render(w, h, integ, 0, eye, rot, max_bounce=mb)
+            parity.assert_parity(g.reshape(-1, 4), o.reshape(-1, 4), f"env/{integ}{mb}/{name}")
