@@ -219,6 +219,10 @@ struct RenderParams {
   // binStart[t+1] index binTris; null = every camera ray walks the BVH
   const int* binStart;
   const int* binTris;
+  // per bin entry: its triangle's geometry record (4 float4) and reference leaf box (2 float4),
+  // gathered at bin build so the camera-ray pass stages a tile's bin in one round trip
+  const float4* binGeo;
+  const float4* binBox;
   int binTilesX, binTilesY;
   // camera-ray pass (primaryKernel): per pixel (py * width + px) the camera ray's result,
   // {tri, t bits}: tri >= 0 a hit, PRIM_MISS (finished: sky colour written), PRIM_RETRACE
@@ -307,13 +311,15 @@ struct PrimaryBins {
   int* tileCount = nullptr;  // per tile: its triangles, then the fill cursors
   int* binStart = nullptr;   // per tile (+1)
   int* binTris = nullptr;
+  float4* binGeo = nullptr;  // per entry: geo[4 tri .. 4 tri + 3] (RenderParams::binGeo)
+  float4* binBox = nullptr;  // per entry: leafBox[2 tri], [2 tri + 1]
   void* tmp = nullptr;       // hipcub scan scratch
   size_t rectCap = 0, triCountCap = 0, triOffsetCap = 0, tileCountCap = 0, binStartCap = 0, binTrisCap = 0,
-         tmpBytes = 0;
+         binGeoCap = 0, binBoxCap = 0, tmpBytes = 0;
   int tilesX = 0, tilesY = 0, entries = 0;
 };
-hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, int height, const float4* geo, int nTri,
-                            PrimaryBins& b, hipStream_t s);
+hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, int height, const float4* geo,
+                            const float4* leafBox, int nTri, PrimaryBins& b, hipStream_t s);
 void freePrimaryBins(PrimaryBins& b);
 
 // The runtime's own tree built on the device (pt_build.hip): a binned-SAH tree

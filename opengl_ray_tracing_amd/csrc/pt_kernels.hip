@@ -405,8 +405,11 @@ __device__ __forceinline__ int primaryPacket(const RenderParams& p, const FrameR
 // every other pixel's result goes to primHit for the megakernel.
 __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   __shared__ float4 s_tri[PT_PASS_BIN_CAP * 4];
+  __shared__ float4 s_box[PT_PASS_BIN_CAP * 2];
   __shared__ int s_idx[PT_PASS_BIN_CAP];
-  // block b: tile b / nFrames of frame b % nFrames (a batch's frames of one tile side by side)
+  // block b: tile b / nFrames of frame b % nFrames (a batch's frames of one tile side by side).
+  // (Blocks of 2 / 4 / 8 such one-wave items, fewer workgroups for the dispatcher: c2's 1/8 share of
+  // a 20-frame batch 88.6 -> 92.2 / 93.4 / 102.2 us; one block per tile for several frames: DESIGN.md 3b.)
   const int fr = (int)(blockIdx.x % (unsigned)p.nFrames);
   const int w = (int)(blockIdx.x / (unsigned)p.nFrames);
   const int lane = threadIdx.x;
@@ -434,10 +437,12 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
     if (valid) *out = make_int2(PRIM_TILE, 0);
     return;
   }
-  for (int t = lane >> 2; t < n; t += 16) {  // one float4 of one triangle per lane
-    const int i = p.binTris[b0 + t];
-    s_tri[4 * t + (lane & 3)] = p.scene.geo[4 * (size_t)i + (lane & 3)];
-    if ((lane & 3) == 0) s_idx[t] = i;
+  // the bin's triangles and their leaf boxes in bin order (binGeo / binBox, gathered at bin build): one
+  // round trip after binStart instead of binTris -> geo, and refReachable's leaf box from LDS
+  for (int t = lane >> 2; t < n; t += 16) {  // one float4 of one triangle (and of its leaf box) per lane
+    s_tri[4 * t + (lane & 3)] = p.binGeo[4 * (size_t)(b0 + t) + (lane & 3)];
+    if ((lane & 3) < 2) s_box[2 * t + (lane & 3)] = p.binBox[2 * (size_t)(b0 + t) + (lane & 3)];
+    else if ((lane & 3) == 2) s_idx[t] = p.binTris[b0 + t];
   }
   __syncthreads();
   uint32_t seed;
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
   uint32_t rays = 0;
   if (valid) {
     int res = best >= 0 ? s_idx[best] : PRIM_MISS;
-    if (tie || (res >= 0 && !refReachable(p.scene, res, eye, dir, tbest))) {
+    if (tie || (res >= 0 && !refReachableBox(p.scene, s_box[2 * best], s_box[2 * best + 1], eye, dir, tbest))) {
       res = PRIM_RETRACE;  // counted by the megakernel's retrace
     } else {
       rays = 1;
@@ -474,7 +479,7 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
 }
 
 hipError_t launchPrimary(const RenderParams& p, hipStream_t s) {
-  if (!p.primHit || !p.binStart || p.numItems <= 0) return hipErrorInvalidValue;
+  if (!p.primHit || !p.binStart || !p.binGeo || !p.binBox || p.numItems <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(primaryKernel, dim3((unsigned)p.numItems * (unsigned)p.nFrames), dim3(64), 0, s, p);
   return hipGetLastError();
 }

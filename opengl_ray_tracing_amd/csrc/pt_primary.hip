@@ -22,6 +22,7 @@
 //   binCountKernel  per (triangle, tile) entry: count the tile's triangles
 //   scan            per-tile counts -> bin starts (hipcub)
 //   binFillKernel   per entry: place the triangle in its tile's bin
+//   binGatherKernel per entry: its triangle's geometry record and leaf box, in bin order
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -126,6 +127,16 @@ __global__ void binFillKernel(const int* offset, const int4* rect, int nTri, int
   binTris[binStart[tile] + atomicAdd(cursor + tile, 1)] = tri;
 }
 
+// per entry: its triangle's geometry record and reference leaf box, next to each other in bin order
+__global__ void binGatherKernel(const int* binTris, int entries, const float4* geo, const float4* leafBox,
+                                float4* binGeo, float4* binBox) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= entries) return;
+  const int i = binTris[e];
+  for (int q = 0; q < 4; q++) binGeo[4 * (size_t)e + q] = geo[4 * (size_t)i + q];
+  for (int q = 0; q < 2; q++) binBox[2 * (size_t)e + q] = leafBox[2 * (size_t)i + q];
+}
+
 // exclusive prefix sum of n ints in place-free form (out may not alias in); the total lands in out[n]
 static hipError_t scanInts(const int* in, int* out, int n, void*& tmp, size_t& tmpBytes, hipStream_t s) {
   size_t need = 0;
@@ -141,8 +152,8 @@ static hipError_t scanInts(const int* in, int* out, int n, void*& tmp, size_t& t
   return hipcub::DeviceScan::ExclusiveSum(tmp, need, in, out, n + 1, s);
 }
 
-hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, int height, const float4* geo, int nTri,
-                            PrimaryBins& b, hipStream_t s) {
+hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, int height, const float4* geo,
+                            const float4* leafBox, int nTri, PrimaryBins& b, hipStream_t s) {
   BinCam c;
   for (int a = 0; a < 3; a++) c.eye[a] = eye[a];
   // columns c0 = cam[0..2], c1 = cam[4..6], c2 = cam[8..10] (column-major, IS:849)
@@ -188,6 +199,11 @@ hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, 
   if (entries > 0)
     hipLaunchKernelGGL(binFillKernel, dim3((entries + B - 1) / B), dim3(B), 0, s, b.triOffset, b.rect, nTri, c.tilesX,
                        entries, b.binStart, b.tileCount, b.binTris);
+  if ((e = grow(b.binGeo, b.binGeoCap, 4 * (size_t)std::max(entries, 1))) != hipSuccess) return e;
+  if ((e = grow(b.binBox, b.binBoxCap, 2 * (size_t)std::max(entries, 1))) != hipSuccess) return e;
+  if (entries > 0 && leafBox)
+    hipLaunchKernelGGL(binGatherKernel, dim3((entries + B - 1) / B), dim3(B), 0, s, b.binTris, entries, geo, leafBox,
+                       b.binGeo, b.binBox);
   b.tilesX = c.tilesX;
   b.tilesY = c.tilesY;
   b.entries = entries;
@@ -196,7 +212,7 @@ hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, 
 
 void freePrimaryBins(PrimaryBins& b) {
   for (void* p : {(void*)b.rect, (void*)b.triCount, (void*)b.triOffset, (void*)b.tileCount, (void*)b.binStart,
-                  (void*)b.binTris, b.tmp})
+                  (void*)b.binTris, (void*)b.binGeo, (void*)b.binBox, b.tmp})
     if (p) (void)hipFree(p);
   b = PrimaryBins{};
 }

@@ -1745,7 +1745,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
         if (int e = waitOthers()) return e;
       }
       ctx->binsValid = false;
-      CK(buildPrimaryBins(eye, cameraRotate, c.width, c.height, ctx->d_geo, ctx->nTri, ctx->bins, S));
+      CK(buildPrimaryBins(eye, cameraRotate, c.width, c.height, ctx->d_geo, ctx->d_leafBox, ctx->nTri, ctx->bins, S));
       std::memcpy(ctx->binEye, eye, sizeof(ctx->binEye));
       std::memcpy(ctx->binCam, cameraRotate, sizeof(ctx->binCam));
       ctx->binVersion = ctx->sceneVersion;
@@ -1763,6 +1763,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     }
     p.binStart = ctx->bins.binStart;
     p.binTris = ctx->bins.binTris;
+    p.binGeo = ctx->bins.binGeo;
+    p.binBox = ctx->bins.binBox;
     p.binTilesX = ctx->bins.tilesX;
     p.binTilesY = ctx->bins.tilesY;
     if (pass) {

@@ -699,8 +699,9 @@ __device__ __forceinline__ void walk4Run(const SceneView& S, V3 o, V3 d, bool an
 // an unreachable w, sends the ray through the reference traversal itself.
 // A miss in the runtime's tree is a miss in the reference's (it meets every
 // triangle the ray hits). An any-hit result stands when its triangle is reachable.
-__device__ __forceinline__ bool refReachable(const SceneView& S, int tri, V3 o, V3 d, float t) {
-  const float4 lo = S.leafBox[2 * (size_t)tri], hi = S.leafBox[2 * (size_t)tri + 1];
+// refReachable with the triangle's leaf box (leafBox[2 tri], [2 tri + 1]) at hand
+__device__ __forceinline__ bool refReachableBox(const SceneView& S, const float4 lo, const float4 hi, V3 o, V3 d,
+                                                float t) {
   const int leaf = __float_as_int(lo.w);  // the triangle's reference leaf (-1: in none)
   if (leaf < 0) return false;
   const V3 P = o + d * t;
@@ -742,6 +743,9 @@ __device__ __forceinline__ bool refReachable(const SceneView& S, int tri, V3 o, 
     if (!(hitAABB(o, inv, S.refBox[2 * (size_t)c], S.refBox[2 * (size_t)c + 1], t0) > 0.0f)) return false;
   }
   return true;
+}
+__device__ __forceinline__ bool refReachable(const SceneView& S, int tri, V3 o, V3 d, float t) {
+  return refReachableBox(S, S.leafBox[2 * (size_t)tri], S.leafBox[2 * (size_t)tri + 1], o, d, t);
 }
 // the runtime's tree as a SceneView for traceRay / tracePacket
 __device__ __forceinline__ SceneView fastView(const SceneView& S) {
