@@ -185,13 +185,14 @@ def test_runtime_tree_equals_reference_tree(request, name, integrator):
 
 def test_tile_splitting_does_not_change_the_image(c4):
     """Long-path tiles split into smaller work items (frames 4-10 after a restart, while the
-    runtime probes the split policy) only regroup lanes: the image equals the fixed-order,
-    one-item-per-tile one bit for bit, with the same rays, and splitting did happen."""
-    from opengl_ray_tracing_amd import FLAG_NO_TILE_ORDER
+    runtime probes the split policy; frames issued serially -- launches that batch frames never
+    split) only regroup lanes: the image equals the fixed-order, one-item-per-tile one bit for bit,
+    with the same rays, and splitting did happen."""
+    from opengl_ray_tracing_amd import FLAG_NO_TILE_ORDER, FLAG_SERIAL_FRAMES
     cfg, tris, nodes, hdr = c4
     eye, rot = orbit_camera(*cfg.camera)
     split_seen = 0
-    with Renderer(W, H, cfg.integrator, max_bounce=cfg.max_bounce) as r:
+    with Renderer(W, H, cfg.integrator, max_bounce=cfg.max_bounce, flags=FLAG_SERIAL_FRAMES) as r:
         r.upload_scene(tris, nodes)
         r.upload_env(hdr)
         for f in range(12):
