@@ -14,6 +14,10 @@
 #   tune:CFG,FRAMES,ROUNDS,V... A/B of tuning builds (tools/tune.py)
 #   bench[:ARGS]                bench.py with ARGS (spaces as '+'), default --steps 20 --warmup 5
 #   pytest:EXPR                 the GPU suite restricted to -k EXPR
+#   sq:CFG                      where the bench kernels' wave-cycles go (tools/gpu_sq_pass.sh)
+#   attr:CFG,VARIANT...         DRAM-side bytes per frame per build (tools/gpu_attr.sh; tools/attr.py)
+#   evidence                    the default bench line (as the driver runs it), phases of c2/c5,
+#                               shares of c2/c4 over 20 and 200 frames
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -50,6 +54,12 @@ step() {
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$arg" \
         > "gpurun_out/pytest_k.log" 2>&1 || return $?
       tail -3 gpurun_out/pytest_k.log ;;
+    sq) bash tools/gpu_sq_pass.sh "${A[0]:-c2}" ;;
+    attr) bash tools/gpu_attr.sh "${A[@]}" ;;
+    evidence)
+      timeout -k 10 900 python bench.py > gpurun_out/bench_default.log 2>&1 || return $?
+      tail -c 300 gpurun_out/bench_default.log
+      for s2 in phases:c2,c5 shard:c2,20 shard:c2,200 shard:c4,20 shard:c4,200; do step "$s2" || return $?; done ;;
     *) echo "unknown step $name"; return 2 ;;
   esac
 }
