@@ -1613,7 +1613,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // 20 frames from an idle GPU, one rank's share of an N-way split (profiles/r4/shard_time_h20.jsonl,
   // 2 runs each): c2 N = 4 0.129-0.130 -> 0.072 ms per frame, N = 8 0.061 -> 0.046-0.048, c4 N = 4
   // 0.137 -> 0.109-0.113; N = 1, 2 and 200-frame runs within run-to-run spread.
-  constexpr int GRID_PCT = 150;
+#ifndef PT_GRID_PCT
+#define PT_GRID_PCT 150
+#endif
+  constexpr int GRID_PCT = PT_GRID_PCT;
   if (piped && D > 1) {
     int others = 0;  // other launches still in flight: the caller streams frames
     for (int k = 0; k < D; k++)
