@@ -1603,18 +1603,19 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // A caller that waits for every frame gets the whole machine for each.
   const int fullGrid = ctx->numCU * nb;
   int grid = fullGrid;
-  // While other frames are in flight, each frame's grid is 150 % of its equal share: a frame
-  // finishing early leaves waves of the others ready to take its place (measured against 100 /
+  // While other frames are in flight, each frame's grid is PT_GRID_PCT % of its equal share: a frame
+  // finishing early leaves waves of the others ready to take its place (round 4, against 100 /
   // 200 / 300 % with the bench line as the driver runs it, 20 frames from an idle GPU: c2 0.285 /
-  // 0.262 / 0.266 / 0.289 ms per frame at 100 / 150 / 200 / 300, c4 0.413 / 0.360 / 0.367 / 0.385).
-  // The share follows the launches actually in flight, 150 % / (1 + the others still running):
+  // 0.262 / 0.266 / 0.289 ms per frame at 100 / 150 / 200 / 300, c4 0.413 / 0.360 / 0.367 / 0.385;
+  // round 5's batched launches prefer 125, PT_GRID_PCT).
+  // The share follows the launches actually in flight, PT_GRID_PCT % / (1 + the others running):
   // a launch issued into a filling pipeline (the first batches after an idle GPU) takes the
-  // machine the earlier ones leave as they drain, and a full pipeline gets 150 % / D each.
+  // machine the earlier ones leave as they drain, and a full pipeline gets PT_GRID_PCT % / D each.
   // 20 frames from an idle GPU, one rank's share of an N-way split (profiles/r4/shard_time_h20.jsonl,
   // 2 runs each): c2 N = 4 0.129-0.130 -> 0.072 ms per frame, N = 8 0.061 -> 0.046-0.048, c4 N = 4
   // 0.137 -> 0.109-0.113; N = 1, 2 and 200-frame runs within run-to-run spread.
 #ifndef PT_GRID_PCT
-#define PT_GRID_PCT 150
+#define PT_GRID_PCT 125  // round 5, final kernels: c4 0.2571 -> 0.2463 ms at 150 -> 125, its 1/8 share 0.0721 -> 0.0688, c2's 0.0332 -> 0.0325; 175: c2 +3 %
 #endif
   constexpr int GRID_PCT = PT_GRID_PCT;
   if (piped && D > 1) {
