@@ -1617,7 +1617,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
 #ifndef PT_GRID_PCT
 #define PT_GRID_PCT 125  // round 5, final kernels: c4 0.2571 -> 0.2463 ms at 150 -> 125, its 1/8 share 0.0721 -> 0.0688, c2's 0.0332 -> 0.0325; 175: c2 +3 %
 #endif
-  constexpr int GRID_PCT = PT_GRID_PCT;
+#ifndef PT_GRID_PCT_WIDE
+#define PT_GRID_PCT_WIDE 150  // large scenes (c5: two frames per launch, ~8 ms launches): 4.44 ms at 125
+#endif
+  const int GRID_PCT = wideScene ? PT_GRID_PCT_WIDE : PT_GRID_PCT;
   if (piped && D > 1) {
     int others = 0;  // other launches still in flight: the caller streams frames
     for (int k = 0; k < D; k++)
