@@ -308,7 +308,10 @@ static int batchFor(const pt_ctx* ctx, bool wideScene) {
 #ifndef PT_BATCH_LAMBERT
 #define PT_BATCH_LAMBERT 12  // c2, 20 frames: 8 + 8 + 4 -> 12 + 8, 0.1789-0.1802 -> 0.1707-0.1729 ms (10: 0.1949); 200 frames equal
 #endif
-  const int m = wideScene ? (fewQueues ? 2 : 1) : c.integrator == 0 ? (fewQueues ? PT_BATCH_LAMBERT : 2) : (fewQueues ? 16 : 4);
+#ifndef PT_BATCH_MIS
+#define PT_BATCH_MIS 16
+#endif
+  const int m = wideScene ? (fewQueues ? 2 : 1) : c.integrator == 0 ? (fewQueues ? PT_BATCH_LAMBERT : 2) : (fewQueues ? PT_BATCH_MIS : 4);
   return std::max(1, std::min(m * std::max(1, c.tile_world), MAX_BATCH));
 }
 
