@@ -106,7 +106,7 @@ typedef struct pt_config {
   int frame_batch;    /* pt_render_frames_async: most frames per launch, at most 32 (0 = automatic:
                          2 x tile_world frames with the Lambert integrator, 4 x tile_world with
                          Disney/MIS, tile_world with Disney/MIS on scenes of more than 48 MB of
-                         records -- 12 x / 16 x / 2 x when the hardware queues allow at most 3
+                         records -- 12 x / 16 x (32 x for MIS beyond 2 bounces) / 2 x when the hardware queues allow at most 3
                          frames in flight, e.g. HIP's default GPU_MAX_HW_QUEUES = 4) */
   int hw_queues;      /* hardware queues of the process's HIP runtime (GPU_MAX_HW_QUEUES in effect when
                          HIP initialised; bounds the frames in flight); 0 = read GPU_MAX_HW_QUEUES now */

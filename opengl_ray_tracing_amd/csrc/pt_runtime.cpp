@@ -301,6 +301,8 @@ const char* pt_last_error(pt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_creat
 // 2 / 4 / 6 / 8 / 12 / 16 frames per launch 0.218 / 0.196 / 0.187 / 0.184 / 0.178 / 0.184 ms per
 // frame; c4 at 4 / 8 / 16 0.342 / 0.302 / 0.271; c5 at 1 / 2 4.59 / 4.34; c2's shares at 20 frames,
 // N = 2 / 4 / 8, at 2 x N 0.116 / 0.066 / 0.041 and 4 x N 0.107 / 0.060 / 0.041 ms).
+static int defaultBounce(int integ);
+
 static int batchFor(const pt_ctx* ctx, bool wideScene) {
   const pt_config& c = ctx->cfg;
   if (c.frame_batch > 0) return std::min(c.frame_batch, MAX_BATCH);
@@ -311,7 +313,15 @@ static int batchFor(const pt_ctx* ctx, bool wideScene) {
 #ifndef PT_BATCH_MIS
 #define PT_BATCH_MIS 16
 #endif
-  const int m = wideScene ? (fewQueues ? 2 : 1) : c.integrator == 0 ? (fewQueues ? PT_BATCH_LAMBERT : 2) : (fewQueues ? PT_BATCH_MIS : 4);
+#ifndef PT_BATCH_MIS_MK
+// MIS beyond its shader's 2 bounces renders on the megakernel (c4): 32 frames per launch, c4 0.2599
+// -> 0.2327 ms over 20 frames (one launch instead of 16 + 4), 0.2389 -> 0.2303 over 100; the MIS
+// regen kernel (c3) keeps 16 (24 / 32: 0.1107 -> 0.1122 / 0.1148)
+#define PT_BATCH_MIS_MK 32
+#endif
+  const int mb = c.max_bounce >= 0 ? c.max_bounce : defaultBounce(c.integrator);
+  const int mis = c.integrator == 2 && mb > 2 ? PT_BATCH_MIS_MK : PT_BATCH_MIS;
+  const int m = wideScene ? (fewQueues ? 2 : 1) : c.integrator == 0 ? (fewQueues ? PT_BATCH_LAMBERT : 2) : (fewQueues ? mis : 4);
   return std::max(1, std::min(m * std::max(1, c.tile_world), MAX_BATCH));
 }
 

@@ -344,7 +344,8 @@ def test_frame_batches_equal_serial_frames(request, name, tile, batch, flags):
     b, sb = run(FLAG_SERIAL_FRAMES, False)
     assert sa.frames == sb.frames == sum(c[2] for c in calls)
     few = sa.frames_in_flight <= 3  # pt_runtime.cpp batchFor: few hardware queues, more frames per launch
-    m = (12 if few else 2) if cfg.integrator == "lambert" else (16 if few else 4)
+    mis = 32 if cfg.max_bounce > 2 else 16  # MIS beyond 2 bounces: the megakernel's batches
+    m = (12 if few else 2) if cfg.integrator == "lambert" else (mis if few else 4)
     auto = min(m * tile[1], 32)
     assert sa.frame_batch == (batch or auto) and sa.launches < sa.frames
     for x, y in zip(a, b):
