@@ -44,8 +44,8 @@ OUT = ROOT / "gpurun_out"
 # --pmc pass -- multiples of every automatic frames-per-launch (1, 2, 4, 8, 16), so the last
 # steps / F dispatches are exactly the timed frames (round 4's first c4 profile at 30 / 10 with F = 4
 # averaged a 2-frame launch in and under-counted its frames by a quarter)
-TRACE_STEPS = 48  # divisible by every frames-per-launch the bench uses (12 for c2, 16 for c4, 2 for c5)
-COUNTER_STEPS = 48
+TRACE_STEPS = 96  # divisible by every frames-per-launch the bench uses (12 for c2, 32 for c4, 2 for c5)
+COUNTER_STEPS = 96
 FRAME_KERNELS = {
     "primary": re.compile(r"primaryKernel"),
     "frame": re.compile(r"renderKernel<\d+, true, false(, \d+)?>|regenKernel<\d+, true[^>]*>"),
