@@ -61,6 +61,7 @@ VALU_PEAK_GINST = 1024 * 2.4 / 2 * 1e9 / 1e9
 METRIC = "Mrays/sec + ms/frame (1 spp, 1080p) at 1/2/4/8 MI355X; CPU-ref spp-matched PSNR"
 PROBE_FRAMES = 90  # frames after a restart during which the renderer measures its policies (tree, split, order, depth)
 SERIAL_FRAMES = 20  # frames of the serial-frames run behind roofline.kernel_basis
+PER_CALLS, PER_CALL_WARMUP = 100, 10  # per_call: SURVEY 8(d)'s median of 100 pt_render_frame calls after 10
 
 
 def parse():
@@ -208,6 +209,30 @@ def main():
         frames(PROBE_FRAMES + args.warmup + args.steps, args.steps, per=1)
         sync_all()
         per_frame_ms = 1e3 * (time.perf_counter() - t4) / args.steps
+    # what the reference's caller gets per display() (ms/frame = the wall time of one
+    # pt_render_frame, median of 100 frames after 10 warm-up frames; INTEGRATION.md binds one call per
+    # display(), OpenglRayTracing/main.cpp:558-603): synchronous single-frame calls continuing the
+    # same running mean, each timed on the host around the call (its ctypes crossing included)
+    per_call = None
+    if n == 1 and PER_CALLS > 0:
+        f0 = PROBE_FRAMES + args.warmup + args.steps
+        for k in range(PER_CALL_WARMUP):
+            r.render_frame(eye, rot, f0 + k)
+        r.reset_stats()
+        ts = []
+        for k in range(PER_CALLS):
+            ta = time.perf_counter()
+            r.render_frame(eye, rot, f0 + PER_CALL_WARMUP + k)
+            ts.append(1e3 * (time.perf_counter() - ta))
+        sp = r.stats()
+        ts.sort()
+        med = float(np.median(ts))
+        rpf = sp.rays / max(sp.frames, 1)
+        per_call = {"ms_median": round(med, 4), "ms_p10": round(ts[len(ts) // 10], 4),
+                    "ms_p90": round(ts[(9 * len(ts)) // 10], 4), "value": round(rpf / (med * 1e-3) / 1e6, 2),
+                    "unit": "Mrays/s", "calls": PER_CALLS, "warmup_calls": PER_CALL_WARMUP,
+                    "kernel_ms": round(sp.kernel_ms_total / max(sp.launches, 1), 4),
+                    "what": "one synchronous pt_render_frame per display(), frames issued one at a time"}
     # interactive cost after a camera move (the reference's mouse() rotates the camera and zeroes
     # frameCounter, OpenglRayTracing/main.cpp:611-634): frames 0..PROBE_FRAMES-1 of a restarted
     # running mean from a camera rotated by one degree, timed like the steps -- the camera-ray
@@ -328,6 +353,8 @@ def main():
         }
         if combined_finite is not None:
             line["config"]["combined_image_finite"] = combined_finite
+        if per_call is not None:
+            line["per_call"] = per_call
         if per_frame_ms is not None:  # the same frames with a gather after every frame
             line["gather_every_frame"] = {"ms_per_step": round(per_frame_ms, 4),
                                           "value": round(rays_total / (per_frame_ms * 1e-3 * args.steps) / 1e6, 2),

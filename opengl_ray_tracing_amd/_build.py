@@ -107,14 +107,16 @@ def build_variant(name: str, defines: dict, hip_flags=()) -> Path:
     out_dir.mkdir(parents=True, exist_ok=True)
     dflags = [f"-D{k}={v}" for k, v in defines.items()]
     inc = [f"-I{INCLUDE}", f"-I{CSRC}"]
-    objs = []
+    objs, cmds = [], []
     for obj, (kind, src, deps) in SOURCES.items():
         out = out_dir / obj
         objs.append(out)
         if kind == "hip":
-            _run([HIPCC, *HIP_FLAGS, *hip_flags, *dflags, *inc, "-c", str(src), "-o", str(out)])
+            cmds.append([HIPCC, *HIP_FLAGS, *hip_flags, *dflags, *inc, "-c", str(src), "-o", str(out)])
         else:
-            _run(["g++", *CXX_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
+            cmds.append(["g++", *CXX_FLAGS, *dflags, *inc, "-c", str(src), "-o", str(out)])
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        list(ex.map(_run, cmds))
     lib = variant_lib(name)
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(lib), *map(str, objs), "-ldl"])
     return lib

@@ -67,6 +67,11 @@ static constexpr int MAX_BATCH = PT_MAX_BATCH;  // most frames per launch (pt_re
 // running-mean update of the previous frame on another slot (two cross-queue hops), and an N = 8
 // share of c2 kept only ~3 of its 8 frames in flight
 static constexpr int COLS = 2 * MAX_SLOTS + 1;
+// a launch of one frame while nothing else is in flight mixes its samples into the running mean in
+// its own kernels (renderOne: no colour buffer, no mixKernel launch)
+#ifndef PT_DIRECT_SOLO
+#define PT_DIRECT_SOLO 1
+#endif
 static_assert(PT_PIPE >= 1 && PT_PIPE <= PIPE, "PT_PIPE: 1..MAX_SLOTS");
 static_assert(PIPE * NUM_QUEUES * CTL_LINE_INTS * 4 <= (int)CTL_STATS, "queue counters of every slot fit the control block");
 
@@ -1436,7 +1441,8 @@ static int ensureOverflow(pt_ctx* ctx, size_t threads, int* ovfDepth, int ldsDep
 // pays for the probe's slower trial frames; every restart still clears the
 // per-tile split state and cost estimates. Sets *useFast; returns the split
 // percentage for this frame's reorder (0 = off).
-static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast) {
+static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fastAllowed, bool* useFast, int slot,
+                       hipStream_t S) {
   *useFast = fastAllowed;
   ctx->tagSlot = -1;
   if (!ordered) return 0;
@@ -1451,18 +1457,29 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
     }
     const bool keep = ctx->treeDecided >= 0 && ctx->splitDecided >= 0 && ctx->probedKey == ctx->policyKey;
     if (!keep) ctx->treeDecided = ctx->splitDecided = -1;
-    // Frames batched per launch (pipelined, RenderParams::nFrames): no tile splitting. A batch's
-    // launch holds each tile once per frame, so a costly tile's frames already run side by side, and
-    // split items' idle lanes only cost issue slots: c4 without splitting 0.262 -> 0.251 ms at N = 1,
-    // its 1/8 share 0.075 -> 0.070 ms (20 frames) and 0.054 -> 0.048 (200 frames, split at 50 %)
-    if (ctx->pipe && ctx->batchCap > 1) ctx->splitDecided = 0;
+    // Frames batched per launch (pipelined, RenderParams::nFrames) are not split. A batch's launch
+    // holds each tile once per frame, so a costly tile's frames already run side by side, and split
+    // items' idle lanes only cost issue slots: c4 without splitting 0.262 -> 0.251 ms at N = 1, its
+    // 1/8 share 0.075 -> 0.070 ms (20 frames) and 0.054 -> 0.048 (200 frames, split at 50 %). A launch
+    // of one frame (a display() call) is split when the probe found it faster.
+    // (launchReorder applies the split only to launches of one frame, renderOne)
     ctx->probedKey = ctx->policyKey;
-    // split state and cost estimates start over (the camera or scene changed), in
-    // every slot's stream order (after its last reorder, before its next frame)
+    // split state and cost estimates start over (the camera or scene changed), in every slot's
+    // stream order (after its last reorder, before its next frame): this launch's slot on the stream
+    // S it runs on (which may be the caller's, renderOne's solo launch), every other slot on its own
+    // stream, with that slot's kernelDone recorded after the reset so that a later launch of the
+    // slot issued solo on the caller's stream (only once every kernelDone has completed) follows it
     if (ctx->d_cost)
-      for (int k = 0; k < (ctx->pipe ? ctx->pipeDepth : 1); k++)
+      for (int k = 0; k < (ctx->pipe ? ctx->pipeDepth : 1); k++) {
+        const bool own = k == slot || !ctx->pipe;
+        hipStream_t sk = own ? S : ctx->slotStream[k];
         (void)hipMemsetAsync(ctx->d_cost + (size_t)k * 4 * ctx->numItems + 2 * (size_t)ctx->numItems, 0,
-                             2 * (size_t)ctx->numItems * sizeof(int), ctx->pipe ? ctx->slotStream[k] : ctx->stream);
+                             2 * (size_t)ctx->numItems * sizeof(int), sk);
+        if (!own && ctx->kernelDone[k]) {
+          (void)hipEventRecord(ctx->kernelDone[k], sk);
+          ctx->slotBusy[k] = true;
+        }
+      }
   }
   const int f = ctx->probeFrame < 1000 ? ctx->probeFrame++ : 1000;
   auto avg = [&](int k) { return ctx->probeN[k] ? ctx->probeMs[k] / ctx->probeN[k] : 1e30; };
@@ -1716,7 +1733,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // not to) and the split policy: probePolicy
   bool useFast = false;
   const int splitPct = probePolicy(ctx, frameCounter, ordered,
-                                   !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast);
+                                   !count && !regen && ctx->fastReady && !(c.flags & PT_FLAG_REFERENCE_TREE), &useFast,
+                                   slot, S);
   // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
   if (regen && walk4) useFast = true;
   if (regen && wide)  // its own LDS copy's size: the top of the tree, or all of it
@@ -1730,6 +1748,14 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const int nF = piped && !probing ? std::max(1, std::min(want, ctx->batchCap)) : 1;
   if (done) *done = nF;
   p.nFrames = nF;
+  // One megakernel frame issued while no other launch is in flight (a display() call, SURVEY 8(d)'s
+  // per-call time): the kernel mixes each pixel's sample into the running mean itself (IS:868-871;
+  // one writer per pixel, the previous frame's update is ordered before it on the caller's stream)
+  // -- no colour buffer round trip and no running-mean update launch: c4 per call 0.785 -> 0.772 ms.
+  // The regen kernel keeps the update launch: the read of the running mean at each path's end stalls
+  // its lock-step waves (c2 0.455 either way, c3 0.578 -> 0.587 ms)
+  const bool direct = piped && solo && nF == 1 && !regen && PT_DIRECT_SOLO;
+  if (direct && ctx->mixPending && ctx->lastMixStream != S) CK(hipStreamWaitEvent(S, ctx->mixDone[ctx->lastCol], 0));
   p.sampleStride = c.sample_world > 0 ? (uint32_t)c.sample_world : 1u;
   // per-frame buffers indexed by the pixel's slot in this context's share (shareIndex): a 1/N share's
   // colour and camera-ray buffers are 1/N of a frame (c5 at N = 8, 16 frames per launch: ~2.4 GB of
@@ -1755,7 +1781,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     CK(hipMalloc(&ctx->d_col[colIdx], (size_t)cap * shareN * sizeof(float4)));
     ctx->colCap[colIdx] = cap;
   }
-  p.col = piped ? ctx->d_col[colIdx] : nullptr;
+  p.col = piped && !direct ? ctx->d_col[colIdx] : nullptr;
   p.packets = PT_PACKETS && (p.scene.fast ? ctx->fDepth : ctx->depth) + 1 <= PKT_DEPTH;
   // camera-ray bins, rebuilt when the camera or the scene changed (the previous frame
   // has ended first: it may still read the old bins); they need the reference facts
@@ -1861,7 +1887,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
 #endif
   if (ordered) {
     CK(launchReorder(cost, cost + ctx->numItems, cost + 2 * (size_t)ctx->numItems, cost + 3 * (size_t)ctx->numItems,
-                     order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitPct, S));
+                     order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), nF > 1 ? 0 : splitPct, S));
     ctx->orderValid[slot] = true;
   }
   // kernel_ms: the frame's own kernels (camera-ray pass, frame kernel, reorder), so the
@@ -1877,9 +1903,10 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     if (ctx->mixPending && ctx->lastMixStream != ctx->stream)  // the caller switched streams: keep frame order
       CK(hipStreamWaitEvent(ctx->stream, ctx->mixDone[ctx->lastCol], 0));
     ctx->lastMixStream = ctx->stream;
-    CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[colIdx], shareN, nF,
-                 frameCounter, ctx->stream));
-    CK(hipEventRecord(ctx->mixDone[colIdx], ctx->stream));
+    if (!direct)
+      CK(launchMix(packParams(ctx, c.tile_rank, c.tile_world), ctx->d_accum, ctx->d_col[colIdx], shareN, nF,
+                   frameCounter, ctx->stream));
+    CK(hipEventRecord(ctx->mixDone[colIdx], ctx->stream));  // direct: the frame's kernels updated it
     ctx->lastSlot = slot;
     ctx->lastCol = colIdx;
     ctx->mixPending = true;

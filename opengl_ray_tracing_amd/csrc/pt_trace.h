@@ -882,6 +882,10 @@ __device__ __forceinline__ int itemLg(int item) { return (item >> 28) & 7; }
 // A batch of nFrames frames (RenderParams::nFrames): claim `it` of queue q is work item
 // it / nFrames of the band for frame it % nFrames, so a band's claims cover its items once
 // per frame and the frames of one item are claimed one after another (set in *frame).
+// (Round 6, a display() call's single frame: probing every queue not yet found empty in one round
+// trip once the home queue drains -- 31 lanes, one counter each -- made c2 per call 0.455 -> 0.554
+// ms: the probes of 4096 draining waves hammer every counter line at once. An agent-scope load
+// instead of the atomic is served stale from the XCD's L2, 0.78 ms.)
 struct TileCursor {
   int qi = 0;  // queues found empty (wave-uniform)
   __device__ __forceinline__ int next(int* queue, int perQueue, int numItems, int home, int& frame, int nFrames = 1,
