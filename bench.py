@@ -265,11 +265,16 @@ def main():
             rs.synchronize()
             ss = rs.stats()
             serial_ms = ss.kernel_ms_total / max(ss.launches, 1)
-    combined_finite = None
-    if gather is not None and args.gather == "display":  # the running means to rank 0, once (not timed)
-        gather.gather_accum()
+    combined_finite = combined_filled = None
+    if gather is not None:  # rank 0's accumulation: every rank's running means (not timed)
+        if args.gather == "display":  # the running means to rank 0, once
+            gather.gather_accum()
+        gather.synchronize()
+        r.synchronize()
         if rank == 0:
-            combined_finite = bool(np.isfinite(r.accum()).all())
+            a = r.accum()
+            combined_finite = bool(np.isfinite(a).all())
+            combined_filled = round(float((a[..., 3] == 1.0).mean()), 4)  # every pixel mixed (alpha 1) at least once
     if combine is not None:  # the ranks' running means -> one image on rank 0 (after the timed steps)
         img = combine()
         torch.cuda.synchronize()
@@ -353,6 +358,8 @@ def main():
         }
         if combined_finite is not None:
             line["config"]["combined_image_finite"] = combined_finite
+        if combined_filled is not None:
+            line["config"]["combined_image_filled"] = combined_filled
         if per_call is not None:
             line["per_call"] = per_call
         if per_frame_ms is not None:  # the same frames with a gather after every frame

@@ -225,11 +225,12 @@ __device__ __forceinline__ float2 decodeCache4(uint32_t v, int w, int h) {
 #ifndef PT_DIAG_ENV_SMALL
 #define PT_DIAG_ENV_SMALL 0
 #endif
-__device__ __forceinline__ float4 envTexel(const Env& e, float u, float v) {
-  const int k = texIndex(e.w, e.h, u, v) & ((PT_DIAG_ENV_SMALL & 1) ? 1023 : -1);
+__device__ __forceinline__ float4 envTexelK(const Env& e, int k) {
+  k &= (PT_DIAG_ENV_SMALL & 1) ? 1023 : -1;
   if (e.nt) return e.hdr8 ? decodeHdr8(ldStream(e.hdr8 + k)) : ldStream(e.hdr + k);
   return e.hdr8 ? decodeHdr8(e.hdr8[k]) : e.hdr[k];
 }
+__device__ __forceinline__ float4 envTexel(const Env& e, float u, float v) { return envTexelK(e, texIndex(e.w, e.h, u, v)); }
 // SampleSphericalMap IS:175-181 / toSphericalCoord IS:638-644
 __device__ __forceinline__ void toSpherical(V3 v, float& u, float& w) {
   float a = ptm_atan2f(v.z, v.x), b = ptm_asinf(v.y);
@@ -240,12 +241,38 @@ __device__ __forceinline__ void toSpherical(V3 v, float& u, float& w) {
   u = a;
   w = 1.0f - b;
 }
+// The texel of toSpherical(v) (v normalized) under GL_NEAREST / CLAMP_TO_EDGE, as computed with the
+// correctly rounded atan2 / asin -- decided by their float approximations (include/pt_fmath.h
+// ptm_*_fast, at most 4 / 3 ulp) whenever the approximate texel coordinates lie farther from a
+// texel edge than the approximation can move them (4e-7 of the map's size: the bound from those ulps
+// through toSpherical's float operations is 3e-7, the largest difference measured over 4e6 random
+// directions 1.2e-7), else by the correctly rounded functions themselves. The same texel either way;
+// c2's sky lookups (every camera ray and bounce ray that escapes) at the float functions' cost
+// (c2 0.189 -> ~0.174 ms per frame)
+// (the correctly rounded fallback: a call, so its double-precision registers are not the caller's)
+__device__ __noinline__ int sphTexelExact(int W, int H, V3 v) {
+  float u, w;
+  toSpherical(v, u, w);
+  return texIndex(W, H, u, w);
+}
+__device__ __forceinline__ int sphTexel(int W, int H, V3 v) {
+  float a = ptm_atan2f_fast(v.z, v.x), b = ptm_asinf_fast(v.y);
+  a = a / (2.0f * PT_PI);
+  b = b / PT_PI;
+  a = a + 0.5f;
+  b = b + 0.5f;
+  const float fx = a * (float)W, fy = (1.0f - b) * (float)H;
+  if (fabsf(fx - rintf(fx)) > 4e-7f * (float)W && fabsf(fy - rintf(fy)) > 4e-7f * (float)H) {
+    const int x = (int)fminf(fmaxf(floorf(fx), 0.0f), (float)(W - 1));
+    const int y = (int)fminf(fmaxf(floorf(fy), 0.0f), (float)(H - 1));
+    return y * W + x;
+  }
+  return sphTexelExact(W, H, v);
+}
 // sampleHdr IS:184-189 (clamped at 10)
 __device__ __forceinline__ V3 sampleHdr(const Env& e, V3 v) {
   if (!e.hdr) return v3(0, 0, 0);
-  float u, w;
-  toSpherical(normalize(v), u, w);
-  float4 c = envTexel(e, u, w);
+  float4 c = envTexelK(e, sphTexel(e.w, e.h, normalize(v)));
   return v3(fminf(c.x, 10.0f), fminf(c.y, 10.0f), fminf(c.z, 10.0f));
 }
 // hdrColor IS:647-651 (unclamped)
@@ -271,17 +298,38 @@ __device__ __forceinline__ float2 hdrCacheTexel(const Env& e, float xi1, float x
   if (e.nt) return e.cache4 ? decodeCache4(ldStream(e.cache4 + k), e.w, e.h) : ldStream(e.cache + k);
   return e.cache4 ? decodeCache4(e.cache4[k], e.w, e.h) : e.cache[k];
 }
+#ifndef PT_ENV_TRIG
+#define PT_ENV_TRIG 1  // SampleHdr's sines and cosines from Env::trig when the table is compact
+#endif
+// SampleHdr's angles of a sample-table entry (x, y), IS:576-580
+__device__ __forceinline__ float hdrTheta(float y) { return PT_PI * ((1.0f - y) - 0.5f); }
+__device__ __forceinline__ float hdrPhi(float x) { return 2.0f * PT_PI * (x - 0.5f); }
 __device__ __forceinline__ V3 hdrDirFromCache(float2 c) {
-  float x = c.x, y = c.y;
-  y = 1.0f - y;
-  float phi = 2.0f * PT_PI * (x - 0.5f);
-  float theta = PT_PI * (y - 0.5f);
   float st, ct, sp, cp;
-  ptm_sincosf(theta, &st, &ct);
-  ptm_sincosf(phi, &sp, &cp);
-  return v3(ct * cp, st, ct * sp);
+  ptm_sincosf(hdrTheta(c.y), &st, &ct);
+  ptm_sincosf(hdrPhi(c.x), &sp, &cp);
+  return v3(ct * cp, st, ct * sp);  // IS:583
 }
-__device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2) {
+__device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2, int* entry = nullptr) {
+  // A compact sample table's entries are integers over (w, h) (decodeCache4), so SampleHdr's sines
+  // and cosines take w + h values: Env::trig holds them (envTrigKernel, the same functions of the
+  // same floats), one 8-byte load per angle instead of a double-precision sincos each
+  if (PT_ENV_TRIG && e.trig && (e.cacheRow || e.cache4)) {
+    int col, row;
+    texXY(e.w, e.h, xi1, xi2, col, row);
+    uint32_t v;
+    if (e.cacheRow) {
+      const uint32_t r = e.cacheRow[row];
+      v = (r & 0xffffu) | (uint32_t)e.cacheY[(size_t)(r >> 16) * e.w + col] << 16;
+    } else {
+      const int k = row * e.w + col;
+      v = e.nt ? ldStream(e.cache4 + k) : e.cache4[k];
+    }
+    const float2 t = e.trig[v >> 16], f = e.trig[e.h + 1 + (v & 0xffffu)];
+    if (entry) *entry = (int)(v >> 16) * (e.w + 1) + (int)(v & 0xffffu);
+    return v3(t.y * f.y, t.x, t.y * f.x);
+  }
+  if (entry) *entry = -1;
   return hdrDirFromCache(hdrCacheTexel(e, xi1, xi2));
 }
 // hdrPdf IS:655-666 (sin of the elevation: reference quirk kept)
@@ -312,10 +360,41 @@ __device__ __forceinline__ void hdrColorPdfOf(const Env& e, float4 c, float w, V
   const float p_convert = (float)(e.res * e.res / 2) / (2.0f * PT_PI * PT_PI * sin_theta);
   pdf = p * p_convert;
 }
+// (a call: the correctly rounded atan2 / asin / sin in double precision stay out of the MIS kernels'
+// register allocation -- c5's MIS regen kernel spilled 8 VGPRs with them inlined. Arguments and result
+// by value: an Env or an output passed by reference would live in scratch memory.)
+__device__ __noinline__ float4 hdrColorPdfCall(const uint2* hdr8, const float4* hdr, int w, int h, int res, int nt,
+                                              V3 L) {
+  Env e;
+  e.hdr8 = hdr8;
+  e.hdr = hdr;
+  e.w = w;
+  e.h = h;
+  e.res = res;
+  e.nt = nt;
+  float wv;
+  const float4 c = hdrTexelOf(e, L, wv);
+  V3 color;
+  float pdf;
+  hdrColorPdfOf(e, c, wv, color, pdf);
+  return make_float4(color.x, color.y, color.z, pdf);
+}
 __device__ __forceinline__ void hdrColorPdf(const Env& e, V3 L, V3& color, float& pdf) {
-  float w;
-  const float4 c = hdrTexelOf(e, L, w);
-  hdrColorPdfOf(e, c, w, color, pdf);
+  const float4 r = hdrColorPdfCall(e.hdr8, e.hdr, e.w, e.h, e.res, e.nt, L);
+  color = v3(r.x, r.y, r.z);
+  pdf = r.w;
+}
+// hdrColor and hdrPdf of a light sample's direction (IS:778-779): from Env::light when the sample
+// came from a compact table's entry (sampleHdrDir's *entry) -- the texel's RGBE and the finished pdf,
+// computed at upload by envLightKernel with the operations below -- else computed
+__device__ __forceinline__ void hdrLightColorPdf(const Env& e, int entry, V3 L, V3& color, float& pdf) {
+  if (PT_ENV_TRIG && entry >= 0 && e.light) {
+    const float4 c = decodeHdr8(e.nt ? ldStream(e.light + entry) : e.light[entry]);
+    color = v3(c.x, c.y, c.z);
+    pdf = c.w;
+    return;
+  }
+  hdrColorPdf(e, L, color, pdf);
 }
 
 // ------------------------------------------------------------ BRDF IS:386-711

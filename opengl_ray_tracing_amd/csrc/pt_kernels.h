@@ -176,6 +176,13 @@ struct Env {
   // read 4-byte entries become 639 distinct rows of 2-byte ones (2.6 MB) and a 4 KB row table
   const uint32_t* cacheRow;
   const unsigned short* cacheY;
+  // With the compact table: SampleHdr's (sin, cos) of theta for each y integer 0..h, then of phi
+  // for each x integer 0..w (launchEnvTrig: the device functions of the same floats), null = computed
+  const float2* trig;
+  // With the compact texels too: per sample-table entry (y, x) (index y * (w + 1) + x, x <= w, y <= h)
+  // the light sample's hdrColor and hdrPdf (IS:647-666) of SampleHdr's direction: {the texel's RGBE,
+  // the pdf's bits} (launchEnvLight: the device functions of the same floats), null = computed
+  const uint2* light;
   int w, h, res;        // res = hdrResolution
   // texels read as streaming (non-temporal) loads, so they leave L2 before the scene's lines: on
   // scenes larger than L2 (c5 4.15 vs 4.32 ms per frame with plain loads); on small scenes plain
@@ -355,6 +362,10 @@ hipError_t launchHdrCache(const float* hdr, int w, int h, float4* cache, float* 
 hipError_t launchEnvCompact(const float4* hdr, const float2* cache, int w, int h, uint2* hdr8, uint32_t* cache4,
                             int* bad, hipStream_t s);
 hipError_t launchEnvPack(float4* hdr, const float4* cache, float2* samp, int n, hipStream_t s);
+// Env::trig: (h + 1) + (w + 1) entries
+hipError_t launchEnvTrig(float2* trig, int w, int h, hipStream_t s);
+// Env::light: (w + 1) * (h + 1) entries, from e's compact texels and trig table
+hipError_t launchEnvLight(const Env& e, uint2* light, hipStream_t s);
 hipError_t launchRender(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, bool count,
                         bool wide = false);
 // tile order of the next frame: each queue band's groups of `group` consecutive

@@ -190,14 +190,15 @@ __device__ V3 pathMIS(T& tr, const Env& env, Hit hit, int maxBounce, uint32_t& s
     // (1) light sample IS:772-789
     const float r1 = randf(seed);
     const float r2 = randf(seed);
-    const V3 Ldir = sampleHdrDir(env, r1, r2);
+    int ent;
+    const V3 Ldir = sampleHdrDir(env, r1, r2, &ent);
     if (count) C.texels++;
     const bool tryLight = dot(N, Ldir) > 0.0f;
     V3 lightC = v3(0, 0, 0);
     if (tryLight) {
       V3 color;
       float pdf_light;
-      hdrColorPdf(env, Ldir, color, pdf_light);
+      hdrLightColorPdf(env, ent, Ldir, color, pdf_light);
       const V3 fl = brdfIso(V, N, Ldir, hit.m);
       const float pb = brdfPdf(V, N, Ldir, hit.m);
       const float mis_weight = misWeight(pdf_light, pb);
@@ -1260,6 +1261,44 @@ hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, size
   if (p.count <= 0 || nFrames <= 0) return hipSuccess;
   hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, col, colStride,
                      nFrames, frameCounter);
+  return hipGetLastError();
+}
+// Env::trig: SampleHdr's sines and cosines (IS:582-583) of every integer entry of a compact sample
+// table, by the same device functions of the same floats as hdrDirFromCache
+__global__ void envTrigKernel(float2* trig, int w, int h) {
+  const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (k > w + h + 1) return;
+  float sn, cs;
+  if (k <= h) ptm_sincosf(hdrTheta((float)k / (float)h), &sn, &cs);
+  else ptm_sincosf(hdrPhi((float)(k - h - 1) / (float)w), &sn, &cs);
+  trig[k] = make_float2(sn, cs);
+}
+hipError_t launchEnvTrig(float2* trig, int w, int h, hipStream_t s) {
+  if (!trig || w <= 0 || h <= 0) return hipErrorInvalidValue;
+  const int n = w + h + 2;
+  hipLaunchKernelGGL(envTrigKernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, trig, w, h);
+  return hipGetLastError();
+}
+// Env::light: what a light sample of each sample-table entry reads (IS:778-779), computed once with
+// the operations sampleHdrDir + hdrColorPdf apply to it in a frame
+__global__ void envLightKernel(Env e, uint2* light) {
+  const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (k >= (e.w + 1) * (e.h + 1)) return;
+  const int y = k / (e.w + 1), x = k - y * (e.w + 1);
+  const float2 t = e.trig[y], f = e.trig[e.h + 1 + x];
+  const V3 L = v3(t.y * f.y, t.x, t.y * f.x);
+  float u, w;
+  toSpherical(normalize(L), u, w);
+  const uint2 raw = e.hdr8[texIndex(e.w, e.h, u, w)];
+  V3 color;
+  float pdf;
+  hdrColorPdfOf(e, decodeHdr8(raw), w, color, pdf);
+  light[k] = make_uint2(raw.x, __float_as_uint(pdf));
+}
+hipError_t launchEnvLight(const Env& e, uint2* light, hipStream_t s) {
+  if (!light || !e.trig || !e.hdr8 || e.w <= 0 || e.h <= 0) return hipErrorInvalidValue;
+  const int n = (e.w + 1) * (e.h + 1);
+  hipLaunchKernelGGL(envLightKernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, e, light);
   return hipGetLastError();
 }
 hipError_t launchDisplayPack(const PackParams& p, const float4* accum, float limit, float gamma, uint8_t* packed,

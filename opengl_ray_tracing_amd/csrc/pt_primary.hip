@@ -154,6 +154,9 @@ static hipError_t scanInts(const int* in, int* out, int n, void*& tmp, size_t& t
 
 hipError_t buildPrimaryBins(const float eye[3], const float cam[16], int width, int height, const float4* geo,
                             const float4* leafBox, int nTri, PrimaryBins& b, hipStream_t s) {
+  // the camera-ray pass reads each bin entry's geometry and reference leaf box from the gathered
+  // binGeo / binBox only (binGatherKernel): without leaf boxes it would test unwritten records
+  if (!geo || !leafBox) return hipErrorInvalidValue;
   BinCam c;
   for (int a = 0; a < 3; a++) c.eye[a] = eye[a];
   // columns c0 = cam[0..2], c1 = cam[4..6], c2 = cam[8..10] (column-major, IS:849)

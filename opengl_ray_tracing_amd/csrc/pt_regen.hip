@@ -67,17 +67,9 @@ constexpr int regenTop4W(int waves) { return waves == 3 ? PT_REGEN_TOP4_3 : PT_R
 #ifndef PT_TILE_PRIM
 #define PT_TILE_PRIM 1
 #endif
-// ... and for the MIS kernel too (its tile's results and slots in LDS since round 5; it still
-// spills 36 VGPRs at its 128-VGPR limit with the hand-out's state, so off)
-#ifndef PT_TILE_PRIM_MIS
-#define PT_TILE_PRIM_MIS 0
-#endif
-// the scene's materials staged in LDS per block when there are at most LDS_MATS of them (a hit's
-// material is the second, dependent fetch of its shading: hitRec's material id, then the record)
-#ifndef PT_LDS_MATS
-#define PT_LDS_MATS 0
-#endif
-constexpr int LDS_MATS = 16;
+// (The MIS kernel keeps the per-lane load: at its 128-VGPR limit it spilled 36 more VGPRs with the
+// hand-out's state; materials staged in LDS per block measured c2 -0.6 %, within noise. Both knobs
+// were deleted in round 6, git history keeps them.)
 
 enum : int { K_NONE = 0, K_PRIMARY = 1, K_BOUNCE = 2, K_SHADOW = 3 };
 
@@ -188,13 +180,14 @@ __device__ __forceinline__ bool continueFromHit(const RenderParams& p, PathState
   V3 N = hit.N;
   float r1 = randf(s.seed);
   float r2 = randf(s.seed);
-  V3 Ldir = sampleHdrDir(p.env, r1, r2);
+  int ent;
+  V3 Ldir = sampleHdrDir(p.env, r1, r2, &ent);
   bool shadow = false;
   if (dot(N, Ldir) > 0.0f) {  // IS:775-790; added if the shadow ray escapes
     V3 L = Ldir;
     V3 color;
     float pdf_light;
-    hdrColorPdf(p.env, L, color, pdf_light);
+    hdrLightColorPdf(p.env, ent, L, color, pdf_light);
     V3 f_r = brdfIso(V, N, L, hit.m);
     float pdf_brdf = brdfPdf(V, N, L, hit.m);
     float mis_weight = misWeight(pdf_light, pdf_brdf);
@@ -307,9 +300,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
     RenderParams p) {
   static_assert(!FULL || W4, "the LDS tree is the 4-wide one");
   static_assert(!FULL || PT_REGEN_YIELD > 0, "the whole LDS tree is walked by walk4Run (loadNode4Lds) only");
-  constexpr bool TILE_PRIM = PT_TILE_PRIM && (INTEG != 2 || PT_TILE_PRIM_MIS);
+  constexpr bool TILE_PRIM = PT_TILE_PRIM && INTEG != 2;
   __shared__ int s_stack[REGEN_LDS_STACK * BS];
-  __shared__ float4 s_mats[PT_LDS_MATS ? LDS_MATS * MAT_F4 : 1];
   StackT<REGEN_LDS_STACK, BS> st;
   st.init(s_stack, p.ovf, p.ovfDepth);
   st.reset();
@@ -329,18 +321,11 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
     const int n = w4 ? p.scene.f4nTop * W4_F4 : p.scene.nTop * 4;  // the staged tree's own record size
     for (int i = threadIdx.x; i < n; i += BS) s_nodes[i] = src[i];
   }
-  if (PT_LDS_MATS && p.scene.nMats <= LDS_MATS)
-    for (int i = threadIdx.x; i < p.scene.nMats * MAT_F4; i += BS) s_mats[i] = p.scene.mats[i];
   __syncthreads();
   const float4* top = FULL ? s_tree : s_nodes;
 #else
-  if (PT_LDS_MATS && p.scene.nMats <= LDS_MATS) {
-    for (int i = threadIdx.x; i < p.scene.nMats * MAT_F4; i += BS) s_mats[i] = p.scene.mats[i];
-    __syncthreads();
-  }
   const float4* top = nullptr;
 #endif
-  if (PT_LDS_MATS && p.scene.nMats <= LDS_MATS) p.scene.mats = s_mats;
   Counters C = {0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   const int home = blockIdx.x & (NUM_QUEUES - 1);

@@ -133,6 +133,8 @@ struct pt_ctx {
   uint32_t* d_cache4 = nullptr;
   uint32_t* d_cacheRow = nullptr;           // the sample table by rows (pt_kernels.h Env::cacheRow)
   unsigned short* d_cacheY = nullptr;
+  float2* d_trig = nullptr;                  // SampleHdr's sines and cosines (Env::trig)
+  uint2* d_light = nullptr;                  // each sample-table entry's light-sample color and pdf (Env::light)
   int hdrW = 0, hdrH = 0;
   // BASIC shapes, the double image, the replayed random stream
   double* d_shapes = nullptr;
@@ -202,6 +204,7 @@ struct pt_ctx {
   unsigned policyKey = 0, probedKey = ~0u;  // bumped by every scene / env upload; the key the decisions were made for
   int orderCap = 0;        // work items per band in d_order
   bool orderValid[PIPE] = {};
+  bool orderSplit[PIPE] = {};               // the slot's order list holds split items (a one-frame launch built it)
   size_t ovfInts = 0;
   // shards
   int shardSize = 32, shardsX = 0, shardsY = 0, numItems = 0, perQueue = 0;
@@ -494,7 +497,7 @@ void pt_destroy(pt_ctx* ctx) {
   dfree(ctx->d_fbvh); dfree(ctx->d_fbvh4); dfree(ctx->d_fpairs); dfree(ctx->d_fastTri);
   dfree(ctx->d_refParent); dfree(ctx->d_refBox); dfree(ctx->d_leafBox);
   dfree(ctx->d_hdr); dfree(ctx->d_cache); dfree(ctx->d_hdr8); dfree(ctx->d_cache4); dfree(ctx->d_shapes);
-  dfree(ctx->d_cacheRow); dfree(ctx->d_cacheY);
+  dfree(ctx->d_cacheRow); dfree(ctx->d_cacheY); dfree(ctx->d_trig); dfree(ctx->d_light);
   dfree(ctx->d_basicImg); dfree(ctx->d_stream); dfree(ctx->d_offsets); dfree(ctx->d_overruns);
   dfree(ctx->d_accum); dfree(ctx->d_ctl); dfree(ctx->d_ovf); dfree(ctx->d_cost); dfree(ctx->d_order);
   dfree(ctx->d_rays); dfree(ctx->d_t); dfree(ctx->d_tri); dfree(ctx->d_rgb);
@@ -1127,6 +1130,8 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
   dfree(ctx->d_cache4);
   dfree(ctx->d_cacheRow);
   dfree(ctx->d_cacheY);
+  dfree(ctx->d_trig);
+  dfree(ctx->d_light);
   ctx->hdrW = ctx->hdrH = 0;
   if (!hdr) return PT_OK;
   if (w <= 0 || h <= 0) return PT_E_INVALID;
@@ -1162,22 +1167,57 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
     const char* e = std::getenv("PT_ENV_COMPACT");
     return !e || std::atoi(e) != 0;
   }();
+  // (built into locals and handed to the context only once verified: a failure part-way leaves the
+  // float texels serving, never a half-built compact form)
   if (compact && w <= 65535 && h <= 65535) {
+    uint2* hdr8 = nullptr;
+    uint32_t* cache4 = nullptr;
     int* d_bad = nullptr;
-    CK(hipMalloc(&ctx->d_hdr8, n * sizeof(uint2)));
-    CK(hipMalloc(&ctx->d_cache4, n * sizeof(uint32_t)));
-    CK(hipMalloc(&d_bad, sizeof(int)));
-    CK(hipMemsetAsync(d_bad, 0, sizeof(int), ctx->stream));
-    hipError_t e = launchEnvCompact(ctx->d_hdr, ctx->d_cache, w, h, ctx->d_hdr8, ctx->d_cache4, d_bad, ctx->stream);
+    hipError_t e = hipMalloc(&hdr8, n * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&cache4, n * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&d_bad, sizeof(int));
+    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0, sizeof(int), ctx->stream);
+    if (e == hipSuccess) e = launchEnvCompact(ctx->d_hdr, ctx->d_cache, w, h, hdr8, cache4, d_bad, ctx->stream);
     int bad = 1;
     if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    (void)hipFree(d_bad);
-    if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("env compact: ") + hipGetErrorString(e));
-    if (bad) {  // not exact: the float texels serve
-      dfree(ctx->d_hdr8);
-      dfree(ctx->d_cache4);
+    dfree(d_bad);
+    if (e != hipSuccess || bad) {  // not exact (or failed): the float texels serve
+      dfree(hdr8);
+      dfree(cache4);
+      if (e != hipSuccess) return fail(ctx, PT_E_HIP, std::string("env compact: ") + hipGetErrorString(e));
+    } else {
+      ctx->d_hdr8 = hdr8;
+      ctx->d_cache4 = cache4;
     }
+  }
+  if (ctx->d_cache4) {  // SampleHdr's sines and cosines of the compact table's integers (Env::trig)
+    float2* trig = nullptr;
+    hipError_t e2 = hipMalloc(&trig, (size_t)(w + h + 2) * sizeof(float2));
+    if (e2 == hipSuccess) e2 = launchEnvTrig(trig, w, h, ctx->stream);
+    if (e2 == hipSuccess) e2 = hipStreamSynchronize(ctx->stream);
+    if (e2 != hipSuccess) {
+      dfree(trig);
+      return fail(ctx, PT_E_HIP, std::string("env trig: ") + hipGetErrorString(e2));
+    }
+    ctx->d_trig = trig;
+    // ... and every entry's light-sample color and pdf (Env::light)
+    Env e;
+    std::memset(&e, 0, sizeof(e));
+    e.hdr = ctx->d_hdr;
+    e.hdr8 = ctx->d_hdr8;
+    e.trig = ctx->d_trig;
+    e.w = e.res = w;
+    e.h = h;
+    uint2* light = nullptr;
+    e2 = hipMalloc(&light, (size_t)(w + 1) * (h + 1) * sizeof(uint2));
+    if (e2 == hipSuccess) e2 = launchEnvLight(e, light, ctx->stream);
+    if (e2 == hipSuccess) e2 = hipStreamSynchronize(ctx->stream);
+    if (e2 != hipSuccess) {
+      dfree(light);
+      return fail(ctx, PT_E_HIP, std::string("env light: ") + hipGetErrorString(e2));
+    }
+    ctx->d_light = light;
   }
   if (ctx->d_cache4) {
     // the sample table by rows (pt_kernels.h Env::cacheRow), kept when every entry of every row equals
@@ -1200,11 +1240,20 @@ static int envOne(pt_ctx* ctx, const float* hdr, int w, int h, const float* cach
       for (int j = 0; j < w && ok; j++) ok = (row[j] & 0xffffu) == x && (row[j] >> 16) == yr[j];
       rows[i] = x | (uint32_t)id << 16;
     }
-    if (ok) {
-      CK(hipMalloc(&ctx->d_cacheRow, rows.size() * sizeof(uint32_t)));
-      CK(hipMalloc(&ctx->d_cacheY, ys.size() * sizeof(unsigned short)));
-      CK(hipMemcpy(ctx->d_cacheRow, rows.data(), rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-      CK(hipMemcpy(ctx->d_cacheY, ys.data(), ys.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
+    if (ok) {  // both or neither (Env::cacheRow reads cacheY)
+      uint32_t* cr = nullptr;
+      unsigned short* cy = nullptr;
+      hipError_t e = hipMalloc(&cr, rows.size() * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipMalloc(&cy, ys.size() * sizeof(unsigned short));
+      if (e == hipSuccess) e = hipMemcpy(cr, rows.data(), rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(cy, ys.data(), ys.size() * sizeof(unsigned short), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        dfree(cr);
+        dfree(cy);
+        return fail(ctx, PT_E_HIP, std::string("env rows: ") + hipGetErrorString(e));
+      }
+      ctx->d_cacheRow = cr;
+      ctx->d_cacheY = cy;
     }
   }
   ctx->policyKey++;
@@ -1463,6 +1512,9 @@ static int probePolicy(pt_ctx* ctx, uint32_t frameCounter, bool ordered, bool fa
     // 1/8 share 0.075 -> 0.070 ms (20 frames) and 0.054 -> 0.048 (200 frames, split at 50 %). A launch
     // of one frame (a display() call) is split when the probe found it faster.
     // (launchReorder applies the split only to launches of one frame, renderOne)
+#if PT_NO_BATCH_SPLIT_PROBE
+    if (ctx->pipe && ctx->batchCap > 1) ctx->splitDecided = 0;
+#endif
     ctx->probedKey = ctx->policyKey;
     // split state and cost estimates start over (the camera or scene changed), in every slot's
     // stream order (after its last reorder, before its next frame): this launch's slot on the stream
@@ -1684,6 +1736,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
                         (size_t)ctx->hdrW * ctx->hdrH * sizeof(uint32_t) > ((size_t)4 << 20);
   p.env.cacheRow = rowTable ? ctx->d_cacheRow : nullptr;
   p.env.cacheY = rowTable ? ctx->d_cacheY : nullptr;
+  p.env.trig = ctx->d_trig;
+  p.env.light = ctx->d_light;
   p.env.w = ctx->hdrW;
   p.env.h = ctx->hdrH;
   p.env.res = ctx->hdrW;
@@ -1843,7 +1897,8 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   }
   // a frame in band order (probePolicy) records no costs and launches no reorder; the
   // slot's last order list stays valid for its next ordered frame (any list covers every tile)
-  p.tileOrder = ordered && ctx->orderValid[slot] ? order : nullptr;
+  // (a batch does not run the split items a one-frame launch's reorder listed: band order, once)
+  p.tileOrder = ordered && ctx->orderValid[slot] && !(nF > 1 && ctx->orderSplit[slot]) ? order : nullptr;
   p.orderCap = orderCap;
   p.tileCost = ordered ? cost : nullptr;
   p.tileCostMax = ordered ? cost + ctx->numItems : nullptr;
@@ -1889,6 +1944,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     CK(launchReorder(cost, cost + ctx->numItems, cost + 2 * (size_t)ctx->numItems, cost + 3 * (size_t)ctx->numItems,
                      order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), nF > 1 ? 0 : splitPct, S));
     ctx->orderValid[slot] = true;
+    ctx->orderSplit[slot] = nF == 1 && splitPct > 0;
   }
   // kernel_ms: the frame's own kernels (camera-ray pass, frame kernel, reorder), so the
   // policy probe weighs the order's cost too; the running-mean update below is not in it

@@ -30,14 +30,14 @@
 //    texture2D(sampler2D, uv): GL_NEAREST + GL_CLAMP_TO_EDGE (the reference's
 //    sampler state, OpenglRayTracing/main.cpp:184-194): texel (floor(u w),
 //    floor(v h)) clamped to the image, row 0 = the first row uploaded;
-//  * the transcendental built-ins (sin, cos, atan(y, x), asin, log, pow) bound to
-//    include/pt_fmath.h: GLSL leaves their precision to the GL driver, which is
-//    not in the reference; this build defines them there for the oracle and the
-//    GPU alike, so the comparison isolates everything else. sqrt, / and the
-//    rest are IEEE (-ffp-contract=off). A second build (-DREF_GLSL_LIBM=1,
-//    libref_glsl_libm.so) binds them to the host C library's sinf / cosf / atan2f /
-//    asinf / logf / powf instead (glibc: an implementation this repository did not
-//    write), against which the GPU is held to the tolerance bar, not bit equality;
+//  * the transcendental built-ins (sin, cos, atan(y, x), asin, log, pow): GLSL leaves
+//    their precision to the GL driver, which is not in the reference. They are bound
+//    here to the host C library's double-precision sin / cos / atan2 / asin / log / pow
+//    (glibc) rounded to float, i.e. the correctly rounded value in all but rare cases,
+//    computed by code this repository did not write. (Until round 6 they were bound to
+//    include/pt_fmath.h, the functions the GPU itself calls, which made this pin a
+//    self-comparison for every transcendental site.) sqrt, / and the rest are IEEE
+//    (-ffp-contract=off);
 //  * pix, the vertex shader's NDC position (vshader.vsh:7-10) interpolated to the
 //    fragment centre, as the oracle forms it: (2 px + 1) / w - 1 in float.
 #include <cmath>
@@ -57,7 +57,6 @@
 #undef _MSC_EXTENSIONS
 #endif
 
-#include "pt_fmath.h"
 
 using namespace glm;
 
@@ -106,29 +105,16 @@ using glm::min;
 inline float max(int a, float b) { return glm::max((float)a, b); }
 inline float max(float a, int b) { return glm::max(a, (float)b); }
 inline float clamp(float x, int a, int b) { return glm::clamp(x, (float)a, (float)b); }
-#if REF_GLSL_LIBM
-// the second build (oracle/_ref/libref_glsl_libm.so): the host C library's float functions, an
-// implementation independent of include/pt_fmath.h, so the GPU's transcendentals are checked
-// against someone else's arithmetic (tests/test_gpu_libm_pin.py, within SURVEY 8(c)'s bar)
-inline float sin(float x) { return ::sinf(x); }
-inline float cos(float x) { return ::cosf(x); }
-#if REF_GLSL_LIBM == 2  // diagnostics: toSphericalCoord's pair from include/pt_fmath.h
-inline float atan(float y, float x) { return ptm_atan2f(y, x); }
-inline float asin(float x) { return ptm_asinf(x); }
-#else
-inline float atan(float y, float x) { return ::atan2f(y, x); }
-inline float asin(float x) { return ::asinf(x); }
-#endif
-inline float log(float x) { return ::logf(x); }
-inline float pow(float x, float y) { return ::powf(x, y); }
-#else
-inline float sin(float x) { return ptm_sinf(x); }
-inline float cos(float x) { return ptm_cosf(x); }
-inline float atan(float y, float x) { return ptm_atan2f(y, x); }
-inline float asin(float x) { return ptm_asinf(x); }
-inline float log(float x) { return ptm_logf(x); }
-inline float pow(float x, float y) { return ptm_powf(x, y); }
-#endif
+// GLSL's transcendental built-ins: the host C library's double-precision functions (glibc),
+// rounded to float -- the correctly rounded value in all but rare cases, from an implementation
+// this repository did not write (the GPU's include/pt_fmath.h computes the same correctly rounded
+// values its own way; tests/test_fmath.py, tests/test_gpu_libm_pin.py)
+inline float sin(float x) { return (float)::sin((double)x); }
+inline float cos(float x) { return (float)::cos((double)x); }
+inline float atan(float y, float x) { return (float)::atan2((double)y, (double)x); }
+inline float asin(float x) { return (float)::asin((double)x); }
+inline float log(float x) { return (float)::log((double)x); }
+inline float pow(float x, float y) { return (float)::pow((double)x, (double)y); }
 inline float sqrt(float x) { return std::sqrt(x); }
 // a swizzle is a vector wherever GLSL passes one to a built-in
 using glm::normalize;

@@ -11,8 +11,12 @@ records what it computes:
                         16 input / output rows
   glsl/frames.json      per frame case (tests/ref_glsl.py FRAME_CASES): each frame's
                         accumulation (the shader's own main() over every pixel of a
-                        160x90 frame, frames 0..n-1) as a sha256, plus 64 sampled
-                        pixels
+                        160x90 frame, frames 0..n-1) as a sha256, plus 768 sampled
+                        pixels of every frame
+
+The shader text's GLSL transcendentals are glibc's double sin / cos / atan2 / asin /
+log / pow rounded to float (oracle/ref_glsl.cpp): the fixtures are the reference's
+text evaluated with libm code this repository did not write.
 
     python tests/golden/make_glsl_fixtures.py
 """
@@ -32,6 +36,7 @@ import ref_glsl  # noqa: E402
 
 OUT = Path(__file__).resolve().parent / "glsl"
 FUNC_N, FUNC_SEED = 100_000, 1
+SAMPLES = 768  # sampled pixels per frame (of 14 400)
 
 
 def main():
@@ -52,11 +57,13 @@ def main():
         tris, nodes, hdr, cache, eye, rot = ref_glsl.case_inputs(cfg, cam)
         outs = ref_glsl.ref_frames(which, tris, nodes, hdr, cache, eye, rot, nf)
         rng = np.random.default_rng(3)
-        idx = rng.choice(ref_glsl.FRAME_W * ref_glsl.FRAME_H, 64, replace=False)
+        idx = rng.choice(ref_glsl.FRAME_W * ref_glsl.FRAME_H, SAMPLES, replace=False)
         frames.append({"case": name, "shader": which, "integrator": integ, "config": cfg, "camera": list(cam),
                        "frames": nf, "width": ref_glsl.FRAME_W, "height": ref_glsl.FRAME_H,
                        "digests": [ref_glsl.digest(o) for o in outs], "sample_index": idx.tolist(),
-                       "sample_last": ref_glsl.canonical(outs[-1].reshape(-1, 4)[idx]).tolist()})
+                       "sample_last": ref_glsl.canonical(outs[-1].reshape(-1, 4)[idx]).tolist(),
+                       # every frame's sampled pixels, for the GPU's tolerance check (tests/test_gpu_libm_pin.py)
+                       "sample_frames": [ref_glsl.canonical(o.reshape(-1, 4)[idx]).tolist() for o in outs]})
         print(name, [d[:12] for d in frames[-1]["digests"]])
     (OUT / "frames.json").write_text(json.dumps({"generator": "oracle/ref_glsl.cpp ref_glsl_render", "cases": frames}) + "\n")
 
