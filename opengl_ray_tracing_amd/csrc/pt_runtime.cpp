@@ -72,6 +72,10 @@ static constexpr int COLS = 2 * MAX_SLOTS + 1;
 #ifndef PT_DIRECT_SOLO
 #define PT_DIRECT_SOLO 1
 #endif
+// a single frame launched while nothing else is in flight (a display() call) runs on the megakernel
+#ifndef PT_CALL_MEGAKERNEL
+#define PT_CALL_MEGAKERNEL 1
+#endif
 static_assert(PT_PIPE >= 1 && PT_PIPE <= PIPE, "PT_PIPE: 1..MAX_SLOTS");
 static_assert(PIPE * NUM_QUEUES * CTL_LINE_INTS * 4 <= (int)CTL_STATS, "queue counters of every slot fit the control block");
 
@@ -1630,8 +1634,6 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const bool regenAll = !count && cull &&
                         (ctx->regenWide > 0 ||
                          (ctx->regenWide < 0 && (c.integrator == 0 || (c.integrator == 2 && mbounce <= 2))));
-  const bool regen =
-      !count && ((c.flags & PT_FLAG_REGEN) || ((wideScene || regenAll) && !(c.flags & PT_FLAG_MEGAKERNEL)));
   // this frame's stream and per-frame buffers: slot frameNo % depth, colour buffer
   // frameNo % (depth + 1) when pipelined
   const bool piped = ctx->pipe && !count;
@@ -1652,6 +1654,16 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
       if (ctx->slotBusy[k] && hipEventQuery(ctx->kernelDone[k]) == hipErrorNotReady) solo = false;
     (void)hipGetLastError();  // hipEventQuery's not-ready status is not an error
   }
+  // The frame kernel. A single frame issued while nothing else is in flight -- a synchronous
+  // display() call (pt_render_frame), SURVEY 8(d)'s per-call time -- runs on the lock-step megakernel,
+  // which splits its long tiles and orders its work longest first, where the regen kernel's launch
+  // ends in its waves' last paths at falling lane counts: per call c3 0.585 -> 0.373 ms, c2 0.449 ->
+  // 0.439 (c4 is on the megakernel already: 0.78; its regen kernel 1.32). Streams of frames keep
+  // the regen kernel (c2's batches 0.17 ms per frame). PT_FLAG_REGEN pins the regen kernel.
+  const bool oneCall = piped && solo && want == 1 && sceneBytes <= ((size_t)PT_WIDE_SCENE_MB << 20) &&
+                       ctx->regenWide <= 0 && PT_CALL_MEGAKERNEL;
+  const bool regen = !count && ((c.flags & PT_FLAG_REGEN) ||
+                                ((wideScene || (regenAll && !oneCall)) && !(c.flags & PT_FLAG_MEGAKERNEL)));
   hipStream_t S = piped && !solo ? ctx->slotStream[slot] : ctx->stream;
   // every other slot's frame in flight has ended on S (the frames that read buffers
   // rebuilt below)

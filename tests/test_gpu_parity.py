@@ -88,14 +88,19 @@ def test_trace_closest_exact_ties():
     assert np.array_equal(t, t_o)
 
 
-def render_gpu(cfg, tris, nodes, hdr, frames=1, flags=0, integrator=None, max_bounce=None, w=W, h=H):
+def render_gpu(cfg, tris, nodes, hdr, frames=1, flags=0, integrator=None, max_bounce=None, w=W, h=H, stream=False):
+    """frames synchronous display() calls (pt_render_frame), or stream=True: one asynchronous stream of
+    frames (pt_render_frames_async, batched launches)"""
     eye, rot = orbit_camera(*cfg.camera)
     with Renderer(w, h, integrator or cfg.integrator, max_bounce=cfg.max_bounce if max_bounce is None else max_bounce,
                   flags=flags) as r:
         r.upload_scene(tris, nodes)
         r.upload_env(hdr)
-        for f in range(frames):
-            r.render_frame(eye, rot, f)
+        if stream:
+            r.render_frames(eye, rot, 0, frames)
+        else:
+            for f in range(frames):
+                r.render_frame(eye, rot, f)
         return r.accum(), r.stats()
 
 
@@ -155,10 +160,14 @@ def test_frame_kernels_agree(request, name, integrator):
     a, sa = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_REGEN)
     b, sb = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, flags=FLAG_MEGAKERNEL)
     d, sd = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb)
-    # the regen kernel by default: Lambert, and MIS at its shader's own 2 bounces (pt_runtime.cpp regenAll)
-    assert sb.regen == 0 and sd.regen == (1 if integrator == "lambert" or (integrator == "mis" and mb <= 2) else 0)
+    e, se = render_gpu(cfg, tris, nodes, hdr, frames=2, integrator=integrator, max_bounce=mb, stream=True)
+    # streams of frames run the regen kernel by default for Lambert and MIS at its shader's own 2
+    # bounces (pt_runtime.cpp regenAll); a synchronous display() call's single frame the megakernel
+    assert sb.regen == 0 and sd.regen == 0
+    assert se.regen == (1 if integrator == "lambert" or (integrator == "mis" and mb <= 2) else 0)
     assert np.array_equal(a, b)
     assert np.array_equal(d, b)
+    assert np.array_equal(e, b)
     if integrator == "mis":
         # regeneration skips BRDF rays whose pdf is 0 (IS:816 discards them after tracing)
         assert sb.rays >= sa.rays >= 0.95 * sb.rays
