@@ -8,9 +8,10 @@ OpenglRayTracing bunny scene (5k tris) at 1920x1080, Lambert, 2 bounces.
 
 N > 1 ranks (one process per GPU):
   --shard tiles (default, strong scaling: BASELINE north_star's split): every
-      rank renders its 32x32 screen tiles of the one frame, in batches of
-      2 x tile_world frames per launch (pt_render_frames_async: each frame 1 spp and
-      its own running-mean update, about two whole images' work per launch);
+      rank renders its 32x32 screen tiles of the one frame, in batches of frames per
+      launch (pt_render_frames_async: each frame 1 spp and its own running-mean update;
+      the renderer's batchFor: 12 x N for Lambert at the box's 4 hardware queues, at
+      most 32);
       after every batch the running means of the rank's pixels (f32 radiance,
       12 B/pixel) are gathered to rank 0 over RCCL (bit-exact reassembly),
       pipelined one batch deep: batch b's gather runs on a communication stream
@@ -27,13 +28,15 @@ N > 1 ranks (one process per GPU):
 Rank 0 prints one JSON line (contract in the task statement), with
 ``roofline`` for a frame: the work the hardware counters measured for every kernel
 of a frame (camera-ray pass, frame kernel, tile reorder, running-mean update: VALU
-wave-instructions, DRAM-side bytes; committed under profiles/r4/counters.json by
+wave-instructions, DRAM-side bytes; committed under profiles/<round>/counters.json by
 tools/roofline.py) over this run's live wall time per frame (and, as kernel_basis,
 over the serially issued frames' HIP-event time), against each resource's peak --
 ``bound`` is the resource with the
 highest fraction -- plus ``equivalent_GBs``, the reference algorithm's fetch
 bytes per launch over the same duration; and ``cpu_baseline``
-(the CPU restatement of the reference on the host cores, rank 0 at N = 1).
+(the CPU restatement of the reference on the host cores, rank 0 at N = 1); and ``per_call``
+(N = 1): the median wall time of 100 synchronous pt_render_frame calls after 10 warm-up calls,
+SURVEY 8(d)'s ms/frame -- one display() per call, what INTEGRATION.md's drop-in gets.
 """
 from __future__ import annotations
 
@@ -79,6 +82,7 @@ def parse():
                     help="per-launch PMC counters of the bench kernel per config (tools/roofline.py)")
     ap.add_argument("--no-reset", action="store_true", help="skip the reset_ms_per_frame frames (profiling runs)")
     ap.add_argument("--no-serial", action="store_true", help="skip the serial-frames run (roofline.kernel_basis)")
+    ap.add_argument("--no-per-call", action="store_true", help="skip the per_call run (profiling runs)")
     ap.add_argument("--cpu-all-seconds", type=float, default=4.0,
                     help="cpu_baseline.all_cores sample: full frames at nproc threads for this long (0: skip)")
     ap.add_argument("--flags", type=int, default=0)
@@ -214,7 +218,7 @@ def main():
     # display(), OpenglRayTracing/main.cpp:558-603): synchronous single-frame calls continuing the
     # same running mean, each timed on the host around the call (its ctypes crossing included)
     per_call = None
-    if n == 1 and PER_CALLS > 0:
+    if n == 1 and PER_CALLS > 0 and not args.no_per_call:
         f0 = PROBE_FRAMES + args.warmup + args.steps
         for k in range(PER_CALL_WARMUP):
             r.render_frame(eye, rot, f0 + k)

@@ -162,6 +162,29 @@ __device__ __forceinline__ float2 ldStream(const float2* p) {
   return *p;
 #endif
 }
+// a pipelined frame's sample colour: COL_F = 3 floats per pixel (alpha is always 1, IS:871), 12 bytes
+// written by the frame kernel and read once by mixKernel (16 until round 6: c2 33 -> 25 MB each way)
+__device__ __forceinline__ void stCol(float* p, float r, float g, float b) {
+#if PT_DIAG_NO_STORE
+  if (r != -1234.5f) return;
+#endif
+#if PT_NT_STREAM
+  __builtin_nontemporal_store(r, p);
+  __builtin_nontemporal_store(g, p + 1);
+  __builtin_nontemporal_store(b, p + 2);
+#else
+  p[0] = r;
+  p[1] = g;
+  p[2] = b;
+#endif
+}
+__device__ __forceinline__ float3 ldCol(const float* p) {
+#if PT_NT_STREAM
+  return make_float3(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2));
+#else
+  return make_float3(p[0], p[1], p[2]);
+#endif
+}
 __device__ __forceinline__ void stStream(float4* p, float4 v) {
 #if PT_DIAG_NO_STORE  // diagnostics build (traffic attribution): colours almost never stored
   if (v.x != -1234.5f) return;

@@ -193,8 +193,9 @@ struct Env {
 
 // One frame of a launch as a work item sees it: its sample index (RNG seeds, Sobol
 // index) and its colour buffer (null: the running mean is updated in place).
+constexpr int COL_F = 3;  // floats per pixel of a pipelined frame's colour buffer (r, g, b)
 struct FrameRef {
-  float4* col;
+  float* col;  // COL_F floats per pixel of the share
   uint32_t sampleIndex;
 };
 
@@ -211,7 +212,7 @@ struct RenderParams {
   // Pipelined frames (pt_runtime.cpp "frames in flight"): non-null = write each pixel's
   // sample colour here (float4, w unused) and leave the running mean to mixKernel, which
   // runs in frame order; null = mix into accum in place (IS:868-871)
-  float4* col;
+  float* col;  // COL_F floats per slot of the share
   // A batch of nFrames consecutive frames of one camera in this launch (pt_render_frames_async):
   // frame f draws sample index sampleIndex + f * sampleStride and writes its colours to
   // col + f * colStride and its camera-ray results to primHit + f * colStride, each indexed by the
@@ -237,6 +238,10 @@ struct RenderParams {
   // PRIM_TILE (the tile's bin is over PT_BIN_CAP: the megakernel traces the tile's
   // packet); null = the megakernel traces its camera rays itself
   int2* primHit;
+  // ... compacted per 8x8 wave tile (round 6): tile w of frame f has a 64-bit mask of the slots that
+  // need a path (primMask[f * numItems + w]: not sky, inside the image) and their results in slot
+  // order at primHit + (f * numItems + w) * 64 (primOfSlot); sky slots cost no bytes
+  unsigned long long* primMask;
   int zeroQueue;  // the camera-ray pass zeroes `queue` for the frame kernel after it (no memset)
   int* queue;           // NUM_QUEUES counters (stride CTL_LINE_INTS), zeroed before each launch
   int perQueue;         // items per queue (band), claimed once per frame of the launch
@@ -413,7 +418,7 @@ hipError_t launchUnpack(const PackParams& p, float4* accum, const float* packed,
 // the running-mean updates of nFrames pipelined frames over the rank's owned pixels (PackParams
 // mapping), in frame order: for f = 0 .. nFrames-1, accum = mix(accum, col + f * colStride,
 // 1 / (frameCounter + f + 1)) (IS:868-871, pass2.fsh:15) -- each pixel read and written once
-hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, size_t colStride, int nFrames,
+hipError_t launchMix(const PackParams& p, float4* accum, const float* col, size_t colStride, int nFrames,
                      uint32_t frameCounter, hipStream_t s);
 
 }  // namespace pt

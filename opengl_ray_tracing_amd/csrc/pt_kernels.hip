@@ -273,9 +273,9 @@ __device__ __forceinline__ V3 cameraRay(const RenderParams& p, uint32_t sampleIn
 // f: the frame the pixel belongs to (its sample index and colour buffer)
 __device__ __forceinline__ void accumulate(const RenderParams& p, const FrameRef& f, int px, int py, V3 color, Counters& C,
                                            bool count) {
-  float4* col = f.col;
+  float* col = f.col;
   if (!count && col) {  // pipelined frame: the sample colour, mixed into the running mean in frame order (mixKernel)
-    stStream(col + shareIndex(p, px, py), make_float4(color.x, color.y, color.z, 1.0f));
+    stCol(col + shareIndex(p, px, py) * COL_F, color.x, color.y, color.z);
     return;
   }
   float4* a = p.accum + (size_t)py * p.width + px;
@@ -430,12 +430,16 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
     b1 = p.binStart[ty * p.binTilesX + tx + 1];
   }
   const int n = b1 - b0;
-  int2* out = p.primHit + (size_t)fr * p.colStride + shareIndex(p, px, py);
+  // the tile's results compacted (RenderParams::primMask): the slots that need a path, in slot order
+  int2* out = p.primHit + ((size_t)fr * p.numItems + w) * 64;
+  unsigned long long* mask = p.primMask + (size_t)fr * p.numItems + w;
   FrameRef fp;  // this block's frame (accumulate's colour buffer)
-  fp.col = p.col ? p.col + (size_t)fr * p.colStride : nullptr;
+  fp.col = p.col ? p.col + (size_t)fr * p.colStride * COL_F : nullptr;
   fp.sampleIndex = p.sampleIndex + (uint32_t)fr * p.sampleStride;
   if (n > PT_PASS_BIN_CAP) {  // the frame kernel traces this tile's camera rays (the megakernel as a packet)
-    if (valid) *out = make_int2(PRIM_TILE, 0);
+    const unsigned long long m = __ballot(valid);
+    if (valid) out[__popcll(m & ((1ull << lane) - 1ull))] = make_int2(PRIM_TILE, 0);
+    if (lane == 0) *mask = m;
     return;
   }
   // the bin's triangles and their leaf boxes in bin order (binGeo / binBox, gathered at bin build): one
@@ -463,8 +467,9 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
     }
   }
   uint32_t rays = 0;
+  int res = PRIM_MISS;
   if (valid) {
-    int res = best >= 0 ? s_idx[best] : PRIM_MISS;
+    res = best >= 0 ? s_idx[best] : PRIM_MISS;
     if (tie || (res >= 0 && !refReachableBox(p.scene, s_box[2 * best], s_box[2 * best + 1], eye, dir, tbest))) {
       res = PRIM_RETRACE;  // counted by the megakernel's retrace
     } else {
@@ -474,13 +479,16 @@ __global__ __launch_bounds__(64) void primaryKernel(RenderParams p) {
         accumulate(p, fp, px, py, sampleHdr(p.env, dir), C, false);
       }
     }
-    *out = make_int2(res, __float_as_int(tbest));
   }
+  const bool need = valid && res != PRIM_MISS;
+  const unsigned long long m = __ballot(need);
+  if (need) out[__popcll(m & ((1ull << lane) - 1ull))] = make_int2(res, __float_as_int(tbest));
+  if (lane == 0) *mask = m;
   addRays(p.rayShards, rays);
 }
 
 hipError_t launchPrimary(const RenderParams& p, hipStream_t s) {
-  if (!p.primHit || !p.binStart || !p.binGeo || !p.binBox || p.numItems <= 0) return hipErrorInvalidValue;
+  if (!p.primHit || !p.primMask || !p.binStart || !p.binGeo || !p.binBox || p.numItems <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(primaryKernel, dim3((unsigned)p.numItems * (unsigned)p.nFrames), dim3(64), 0, s, p);
   return hipGetLastError();
 }
@@ -906,7 +914,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
   while (item >= 0) {
     // the item's frame: its sample index and colour buffer (accumulate)
     FrameRef fv;
-    fv.col = p.col ? p.col + (size_t)fr * p.colStride : nullptr;
+    fv.col = p.col ? p.col + (size_t)fr * p.colStride * COL_F : nullptr;
     fv.sampleIndex = p.sampleIndex + (uint32_t)fr * p.sampleStride;
     const int w = itemTile(item);
     const long long t0 = COUNT ? 0 : clock64();
@@ -924,7 +932,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
     const int py = gy * p.shardSize + (s / sub) * 8 + (k >> 3);
     const bool valid = lane < nLanes && px < p.width && py < p.height;
     if (!COUNT && p.primHit) {  // camera rays already traced by primaryKernel
-      const int2 h = valid ? p.primHit[(size_t)fr * p.colStride + shareIndex(p, px, py)] : make_int2(PRIM_MISS, 0);
+      const unsigned long long pm = primTileMask(p, fr, w);
+      const int2 h = valid ? primOfSlot(pm, primTileEntries(p, fr, w), k) : make_int2(PRIM_MISS, 0);
       int tri = h.x;
       float t = __int_as_float(h.y);
       if (__ballot(valid && tri == PRIM_TILE)) {  // wave-uniform: the whole tile
@@ -1129,7 +1138,7 @@ __global__ void unpackRanksKernel(RanksUnpack d, float4* accum) {
 // the running means of a batch of pipelined frames (accumulate's update, deferred to frame
 // order): frame f's colours at col + f * colStride, its weight 1 / (frameCounter + f + 1); the
 // pixel's mean after each frame is the one serial frames store (mixf of the same floats)
-__global__ void mixKernel(PackParams p, float4* accum, const float4* col, size_t colStride, int nFrames,
+__global__ void mixKernel(PackParams p, float4* accum, const float* col, size_t colStride, int nFrames,
                           uint32_t frameCounter) {
   long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= p.count) return;
@@ -1138,7 +1147,7 @@ __global__ void mixKernel(PackParams p, float4* accum, const float4* col, size_t
   const size_t i = (size_t)py * p.width + px;
   float4 a = ldStream(accum + i);
   for (int f = 0; f < nFrames; f++) {
-    const float4 c = ldStream(col + (size_t)f * colStride + k);  // slot k of the share (shareIndex)
+    const float3 c = ldCol(col + ((size_t)f * colStride + k) * COL_F);  // slot k of the share (shareIndex)
     const float w = 1.0f / (float)(frameCounter + (uint32_t)f + 1u);
     a = make_float4(mixf(a.x, c.x, w), mixf(a.y, c.y, w), mixf(a.z, c.z, w), 1.0f);
   }
@@ -1256,7 +1265,7 @@ hipError_t launchPack(const PackParams& p, const float4* accum, float* packed, h
   hipLaunchKernelGGL(packKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, packed);
   return hipGetLastError();
 }
-hipError_t launchMix(const PackParams& p, float4* accum, const float4* col, size_t colStride, int nFrames,
+hipError_t launchMix(const PackParams& p, float4* accum, const float* col, size_t colStride, int nFrames,
                      uint32_t frameCounter, hipStream_t s) {
   if (p.count <= 0 || nFrames <= 0) return hipSuccess;
   hipLaunchKernelGGL(mixKernel, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p, accum, col, colStride,

@@ -98,8 +98,7 @@ __device__ __forceinline__ uint32_t sampleOf(const RenderParams& p, const PathSt
 __device__ __forceinline__ void writeAccum(const RenderParams& p, const PathState& s, V3 color) {
   const int px = s.px, py = s.py;
   if (p.col) {  // pipelined frame: the sample colour; mixKernel updates the running mean in frame order
-    stStream(p.col + (size_t)s.fr * p.colStride + shareIndex(p, px, py),
-             make_float4(color.x, color.y, color.z, 1.0f));
+    stCol(p.col + ((size_t)s.fr * p.colStride + shareIndex(p, px, py)) * COL_F, color.x, color.y, color.z);
     return;
   }
   float4* a = p.accum + (size_t)py * p.width + px;
@@ -336,6 +335,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform; TILE_PRIM: index into s_slot)
   int nValid = 0;     // TILE_PRIM: slots of the tile that need a path (wave-uniform)
   bool drained = false;  // TILE_PRIM: the work queues had nothing left for this wave (wave-uniform)
+  uint32_t tmaskLo = 0, tmaskHi = 0;  // !TILE_PRIM: the claimed tile's camera-ray mask (wave-uniform)
   // TILE_PRIM: the tile's slots that need a path, in slot order, and their camera-ray results (this
   // wave's rows; in LDS rather than registers, which the walk needs)
   __shared__ unsigned char s_slotAll[TILE_PRIM ? BS : 1];
@@ -420,26 +420,30 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
             wTiles++;
             wLastClaim = wall_clock64();
 #endif
-            const int j = tile / p.shardTiles, sI = tile - j * p.shardTiles;
-            const int g = j * p.world + p.rank;
-            const int gy = g / p.shardsX, gx = g - gy * p.shardsX;
-            const int px = gx * p.shardSize + (sI % sub) * 8 + (lane & 7);
-            const int py = gy * p.shardSize + (sI / sub) * 8 + (lane >> 3);
-            const bool in = px < p.width && py < p.height;
-            // without the camera-ray pass every pixel's camera ray is traced here (PRIM_RETRACE)
-            const int2 h = !in ? make_int2(PRIM_MISS, 0)
-                               : p.primHit ? p.primHit[(size_t)tileFr * p.colStride + shareIndex(p, px, py)]
-                                           : make_int2(PRIM_RETRACE, 0);
-            const unsigned long long valid = __ballot(h.x != PRIM_MISS);
-            if (h.x != PRIM_MISS) {
-              const int k = rankBelow(valid);
-              s_slot[k] = (unsigned char)lane;
-              s_hit[k] = h;
+            if (p.primHit) {
+              // the camera-ray pass's compacted results: the tile's mask (scalar), then its first nValid
+              // entries (one coalesced read of 8 bytes per path; sky slots cost nothing)
+              const unsigned long long m = primTileMask(p, tileFr, tile);
+              const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)m);
+              const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
+              if ((lane < 32 ? lo >> lane : hi >> (lane - 32)) & 1u)
+                s_slot[__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u))] = (unsigned char)lane;
+              nValid = __popc(lo) + __popc(hi);
+              if (lane < nValid) s_hit[lane] = primTileEntries(p, tileFr, tile)[lane];
+            } else {  // without the pass every pixel's camera ray is traced here (PRIM_RETRACE)
+              const int px = tilePx(p, tile, sub) + (lane & 7), py = tilePy(p, tile, sub) + (lane >> 3);
+              const bool in = px < p.width && py < p.height;
+              const unsigned long long valid = __ballot(in);
+              if (in) {
+                const int k = rankBelow(valid);
+                s_slot[k] = (unsigned char)lane;
+                s_hit[k] = make_int2(PRIM_RETRACE, 0);
+              }
+              nValid = __popcll(valid);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            nValid = __popcll(valid);
             cursor = 0;
 #if PT_PHASE_STATS
             PH_ADD(18, clock64() - phC);
@@ -498,6 +502,11 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
           if (item < 0) break;  // no tiles left for this wave
           tile = item;
           cursor = 0;
+          if (p.primHit) {  // the tile's mask of the camera-ray pass's compacted results (wave-uniform)
+            const unsigned long long m = primTileMask(p, tileFr, tile);
+            tmaskLo = __builtin_amdgcn_readfirstlane((uint32_t)m);
+            tmaskHi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
+          }
 #if PT_WAVE_TRACE
           wTiles++;
           wLastClaim = wall_clock64();
@@ -508,8 +517,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
           const int px = tilePx(p, tile, sub) + (slot & 7);
           const int py = tilePy(p, tile, sub) + (slot >> 3);
           int2 h = make_int2(0, 0);
-          if (p.primHit && px < p.width && py < p.height)
-            h = p.primHit[(size_t)tileFr * p.colStride + shareIndex(p, px, py)];
+          if (p.primHit)
+            h = primOfSlot((unsigned long long)tmaskHi << 32 | tmaskLo, primTileEntries(p, tileFr, tile), slot);
           if (px < p.width && py < p.height && !(p.primHit && h.x == PRIM_MISS)) {
             s.px = px;
             s.py = py;

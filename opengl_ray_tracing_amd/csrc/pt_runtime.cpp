@@ -194,7 +194,7 @@ struct pt_ctx {
   // every other slot waits for it once before its first frame with those bins (binGen)
   hipEvent_t binsBuilt = nullptr;
   unsigned binGen = 0, binGenSeen[MAX_SLOTS] = {};
-  float4* d_col[COLS] = {};                 // per-colour-buffer sample colours
+  float* d_col[COLS] = {};                  // per-colour-buffer sample colours (COL_F floats per slot)
   int2* d_prim[PIPE] = {};                  // per-slot camera-ray results (primaryKernel)
   int lastSlot = -1;                        // slot of the last pipelined frame
   int lastCol = -1;                         // colour buffer of the last pipelined frame
@@ -1835,7 +1835,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     for (int k = 0; k < nCol; k++)
       if (!ctx->d_col[k]) {
         const int cap = std::max(nF, ctx->batchCap);
-        CK(hipMalloc(&ctx->d_col[k], (size_t)cap * shareN * sizeof(float4)));
+        CK(hipMalloc(&ctx->d_col[k], (size_t)cap * shareN * COL_F * sizeof(float)));
         ctx->colCap[k] = cap;
       }
   if (piped && ctx->colCap[colIdx] < nF) {  // room for the launch's frames (each buffer grows once, to batchCap)
@@ -1844,7 +1844,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
       dfree(ctx->d_col[colIdx]);
     }
     const int cap = std::max(nF, ctx->batchCap);
-    CK(hipMalloc(&ctx->d_col[colIdx], (size_t)cap * shareN * sizeof(float4)));
+    CK(hipMalloc(&ctx->d_col[colIdx], (size_t)cap * shareN * COL_F * sizeof(float)));
     ctx->colCap[colIdx] = cap;
   }
   p.col = piped && !direct ? ctx->d_col[colIdx] : nullptr;
@@ -1888,11 +1888,13 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
     p.binTilesX = ctx->bins.tilesX;
     p.binTilesY = ctx->bins.tilesY;
     if (pass) {
+      // per frame: the share's entries (shareN int2, compacted per wave tile), then its numItems tile masks
+      const size_t primBytes = shareN * sizeof(int2) + (size_t)ctx->numItems * sizeof(unsigned long long);
       if (piped)
         for (int k = 0; k < D; k++)
           if (!ctx->d_prim[k]) {
             const int cap = std::max(nF, ctx->batchCap);
-            CK(hipMalloc(&ctx->d_prim[k], (size_t)cap * shareN * sizeof(int2)));
+            CK(hipMalloc(&ctx->d_prim[k], (size_t)cap * primBytes));
             ctx->primCap[k] = cap;
           }
       if (ctx->primCap[slot] < nF) {  // the slot's previous launch (on S) may still read the old results
@@ -1901,10 +1903,11 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
           dfree(ctx->d_prim[slot]);
         }
         const int cap = std::max(nF, piped ? ctx->batchCap : 1);
-        CK(hipMalloc(&ctx->d_prim[slot], (size_t)cap * shareN * sizeof(int2)));
+        CK(hipMalloc(&ctx->d_prim[slot], (size_t)cap * primBytes));
         ctx->primCap[slot] = cap;
       }
       p.primHit = ctx->d_prim[slot];
+      p.primMask = reinterpret_cast<unsigned long long*>(ctx->d_prim[slot] + (size_t)ctx->primCap[slot] * shareN);
     }
   }
   // a frame in band order (probePolicy) records no costs and launches no reorder; the

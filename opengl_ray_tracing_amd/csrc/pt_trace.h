@@ -924,6 +924,19 @@ __device__ __forceinline__ size_t shareIndex(const RenderParams& p, int px, int 
   return (size_t)j * ss * ss + (size_t)((py - gy * ss) * ss + (px - gx * ss));
 }
 
+// The camera-ray pass's compacted results (RenderParams::primMask / primHit) of wave tile w of frame fr:
+// the tile's mask, its entries, and slot k's result (PRIM_MISS for a slot outside the mask)
+__device__ __forceinline__ unsigned long long primTileMask(const RenderParams& p, int fr, int w) {
+  return p.primMask[(size_t)fr * p.numItems + w];
+}
+__device__ __forceinline__ const int2* primTileEntries(const RenderParams& p, int fr, int w) {
+  return p.primHit + ((size_t)fr * p.numItems + w) * 64;
+}
+__device__ __forceinline__ int2 primOfSlot(unsigned long long m, const int2* e, int slot) {
+  if (!((m >> slot) & 1ull)) return make_int2(PRIM_MISS, 0);
+  return e[__popcll(m & ((1ull << slot) - 1ull))];
+}
+
 // per-wave sum of a lane counter into the block's padded shard
 __device__ __forceinline__ void addRays(unsigned long long* shards, uint32_t r) {
   for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);

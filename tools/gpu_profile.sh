@@ -12,17 +12,17 @@ OUT="$REPO/gpurun_out/prof_${TAG}_${CFG}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 # the bench's own flow: 14 probe frames, W warmup, K timed frames (tools/roofline.py selects those)
-BENCH=(python3 "$REPO/bench.py" --config "$CFG" --steps 96 --warmup 5 --no-cpu-baseline --no-psnr --no-reset --no-serial)
+BENCH=(python3 "$REPO/bench.py" --config "$CFG" --steps 96 --warmup 5 --no-cpu-baseline --no-psnr --no-reset --no-serial --no-per-call)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- "${BENCH[@]}" > "$OUT/bench_line.json" 2> "$OUT/trace.log"; rc=$?
 echo "trace=$rc"; [ $rc -eq 0 ] || exit $rc
 # the same flow with frames issued serially (PT_FLAG_SERIAL_FRAMES = 0x80): the kernel's own duration
-SERIAL=(python3 "$REPO/bench.py" --config "$CFG" --steps 96 --warmup 5 --no-cpu-baseline --no-psnr --no-reset --no-serial --flags 128)
+SERIAL=(python3 "$REPO/bench.py" --config "$CFG" --steps 96 --warmup 5 --no-cpu-baseline --no-psnr --no-reset --no-serial --no-per-call --flags 128)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/serial" -o run -- "${SERIAL[@]}" > "$OUT/serial_line.json" 2> "$OUT/serial.log"; rc=$?
 echo "serial=$rc"; [ $rc -eq 0 ] || exit $rc
 # counters over the bench's own (pipelined) frames: a --pmc pass serialises the dispatches, so each
 # frame kernel's counters -- camera-ray pass, frame kernel, tile reorder, running-mean update --
 # cover its own dispatch (tools/roofline.py sums them per frame)
-BENCHC=(python3 "$REPO/bench.py" --config "$CFG" --steps 96 --warmup 2 --no-cpu-baseline --no-psnr --no-reset --no-serial)
+BENCHC=(python3 "$REPO/bench.py" --config "$CFG" --steps 96 --warmup 2 --no-cpu-baseline --no-psnr --no-reset --no-serial --no-per-call)
 PASSES=(
   "fetch:FETCH_SIZE"
   "write:WRITE_SIZE"
