@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--no-psnr", action="store_true", help="skip the spp-matched PSNR check")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="cpu_baseline sample: full frames are rendered until this much CPU wall time has passed")
-    ap.add_argument("--counters", default=str(ROOT / "profiles" / "r5" / "counters.json"),
+    ap.add_argument("--counters", default=str(ROOT / "profiles" / "r6" / "counters.json"),
                     help="per-launch PMC counters of the bench kernel per config (tools/roofline.py)")
     ap.add_argument("--no-reset", action="store_true", help="skip the reset_ms_per_frame frames (profiling runs)")
     ap.add_argument("--no-serial", action="store_true", help="skip the serial-frames run (roofline.kernel_basis)")
@@ -206,13 +206,15 @@ def main():
     # N > 1: the same steps with one gather per frame (one frame per launch), the cadence at which
     # the reference presents (IS main.cpp:706), timed the same way -- reported next to the batched
     # figure, whose image reaches rank 0 once per batch of `batch` frames
-    per_frame_ms = None
+    per_frame_ms = per_frame_rays = None
     if gather is not None and batch > 1:
         sync_all()
+        r.reset_stats()
         t4 = time.perf_counter()
         frames(PROBE_FRAMES + args.warmup + args.steps, args.steps, per=1)
         sync_all()
         per_frame_ms = 1e3 * (time.perf_counter() - t4) / args.steps
+        per_frame_rays = r.stats().rays  # this window's own rays (other sample indices than the batched window's)
     # what the reference's caller gets per display() (ms/frame = the wall time of one
     # pt_render_frame, median of 100 frames after 10 warm-up frames; INTEGRATION.md binds one call per
     # display(), OpenglRayTracing/main.cpp:558-603): synchronous single-frame calls continuing the
@@ -302,6 +304,9 @@ def main():
             pf = torch.tensor([per_frame_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(pf, op=dist.ReduceOp.MAX)
             per_frame_ms = float(pf[0].item())
+            pr = torch.tensor([float(per_frame_rays)], dtype=torch.float64, device=dev)
+            dist.all_reduce(pr, op=dist.ReduceOp.SUM)
+            per_frame_rays = float(pr[0].item())
         rays_total = float(sm[1].item())
         kernel_ms_avg = float(mx[2].item()) / max(st.launches, 1)
     else:
@@ -368,7 +373,7 @@ def main():
             line["per_call"] = per_call
         if per_frame_ms is not None:  # the same frames with a gather after every frame
             line["gather_every_frame"] = {"ms_per_step": round(per_frame_ms, 4),
-                                          "value": round(rays_total / (per_frame_ms * 1e-3 * args.steps) / 1e6, 2),
+                                          "value": round(per_frame_rays / (per_frame_ms * 1e-3 * args.steps) / 1e6, 2),
                                           "unit": "Mrays/s", "frames_per_gather": 1}
         print(json.dumps(line), flush=True)
     r.close()
