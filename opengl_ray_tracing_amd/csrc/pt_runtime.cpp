@@ -1915,8 +1915,13 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   }
   // a frame in band order (probePolicy) records no costs and launches no reorder; the
   // slot's last order list stays valid for its next ordered frame (any list covers every tile)
+  // Batches of frames run unsplit (probePolicy) -- also on small screen-tile shares, whose launch lasts
+  // about as long as its longest unsplit tile (c4's 1/8 share, 20 frames in one 1.3 ms launch: single
+  // 8x8 tiles of 1.2-1.5 ms): splitting there measured c4 N = 8 0.0726 -> 0.0688 ms per frame over 20
+  // frames but 0.0484 -> 0.0549 over 200, N = 4 0.0867 -> 0.0962 (round 6, not kept)
+  const bool splitThis = nF == 1;
   // (a batch does not run the split items a one-frame launch's reorder listed: band order, once)
-  p.tileOrder = ordered && ctx->orderValid[slot] && !(nF > 1 && ctx->orderSplit[slot]) ? order : nullptr;
+  p.tileOrder = ordered && ctx->orderValid[slot] && !(!splitThis && ctx->orderSplit[slot]) ? order : nullptr;
   p.orderCap = orderCap;
   p.tileCost = ordered ? cost : nullptr;
   p.tileCostMax = ordered ? cost + ctx->numItems : nullptr;
@@ -1960,9 +1965,9 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
 #endif
   if (ordered) {
     CK(launchReorder(cost, cost + ctx->numItems, cost + 2 * (size_t)ctx->numItems, cost + 3 * (size_t)ctx->numItems,
-                     order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), nF > 1 ? 0 : splitPct, S));
+                     order, ctx->perQueue, orderCap, ctx->numItems, group, grid * (BLOCK / 64), splitThis ? splitPct : 0, S));
     ctx->orderValid[slot] = true;
-    ctx->orderSplit[slot] = nF == 1 && splitPct > 0;
+    ctx->orderSplit[slot] = splitThis && splitPct > 0;
   }
   // kernel_ms: the frame's own kernels (camera-ray pass, frame kernel, reorder), so the
   // policy probe weighs the order's cost too; the running-mean update below is not in it

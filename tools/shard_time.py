@@ -62,6 +62,8 @@ def main():
                 g.synchronize()
             r.reset_stats()
             K = int(os.environ.get("PT_SHARD_FRAMES", "200"))  # 20: the driver's bench line, from an idle GPU
+            if os.environ.get("SHARD_TRACE"):  # a PT_WAVE_TRACE build records the timed frames' waves only
+                os.environ["PT_WAVE_TRACE_FILE"] = f"{os.environ['SHARD_TRACE']}_{cfg_name}_n{n}.bin"
             t0 = time.perf_counter()
             frames(100, K)
             t_sub = time.perf_counter()
@@ -69,6 +71,7 @@ def main():
             if g is not None:
                 g.synchronize()
             ms = 1e3 * (time.perf_counter() - t0) / K
+            os.environ.pop("PT_WAVE_TRACE_FILE", None)
             submit_ms = 1e3 * (t_sub - t0) / K  # host time per pt_render_frame_async call
             st = r.stats()
         print(json.dumps({"variant": os.environ.get("PT_VARIANT", "base"), "config": cfg_name, "world": n, "rank0_ms_per_frame": round(ms, 4),
