@@ -877,6 +877,8 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
   Stack st;
   st.init(s_stack, p.ovf, p.ovfDepth);
   st.reset();
+  __shared__ unsigned s_drained;  // the work queues this block's waves found drained (TileCursor)
+  if (threadIdx.x == 0) s_drained = 0;
   // the top of the tree (every ray's first node visits) staged in LDS once per block
 #if PT_LDS_NODES > 0
   __shared__ float4 s_nodes[LDS_NODES * 4];
@@ -890,6 +892,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
   __syncthreads();
   const float4* top = s_nodes;
 #else
+  __syncthreads();
   const float4* top = nullptr;
 #endif
   Counters C = {0, 0, 0, 0, 0};
@@ -904,6 +907,7 @@ __global__ __launch_bounds__(BLOCK, WAVES > 0 ? WAVES
   unsigned long long wTiles = 0, wLongest = 0, wLongestAt = 0, wNodeIt = 0, wLeafIt = 0;
 #endif
   TileCursor cur;
+  cur.drained = &s_drained;
   // Each lane runs its pixel's whole path right after the tile's camera rays.
   // (Deferring the paths of the pixels that hit something to a per-wave LDS
   // queue and running them 64 at a time keeps every lane busy, but it mixes

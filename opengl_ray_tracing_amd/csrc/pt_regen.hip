@@ -304,6 +304,8 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   StackT<REGEN_LDS_STACK, BS> st;
   st.init(s_stack, p.ovf, p.ovfDepth);
   st.reset();
+  __shared__ unsigned s_drained;  // the work queues this block's waves found drained (TileCursor)
+  if (threadIdx.x == 0) s_drained = 0;
   // the top of the tree (every ray's first node visits) -- or all of it -- staged in LDS once per block
 #if PT_LDS_NODES > 0
   constexpr int TOP4 = regenTop4W(WAVES);
@@ -323,6 +325,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   __syncthreads();
   const float4* top = FULL ? s_tree : s_nodes;
 #else
+  __syncthreads();
   const float4* top = nullptr;
 #endif
   Counters C = {0, 0, 0, 0, 0};
@@ -330,6 +333,7 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
   const int home = blockIdx.x & (NUM_QUEUES - 1);
   const int sub = p.shardSize >> 3;
   TileCursor cur;     // wave-uniform
+  cur.drained = &s_drained;
   int tile = -1;      // current 8x8 wave tile (wave-uniform)
   int tileFr = 0;     // its frame in the launch's batch (wave-uniform)
   int cursor = 64;    // next unused pixel slot of the tile (wave-uniform; TILE_PRIM: index into s_slot)
