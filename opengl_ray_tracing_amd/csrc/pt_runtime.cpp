@@ -1725,7 +1725,6 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   int ovfDepth = 0;
   int rc = ensureOverflow(ctx, (size_t)fullGrid * bs, &ovfDepth, regen ? regenLdsStack() : LDS_STACK, D);
   if (rc) return rc;
-  const size_t npix = (size_t)c.width * c.height;
   // the colour buffer's previous launch (nCol back) has been mixed (the slot's queue counters,
   // order list and camera-ray results belong to its previous launch on this same stream)
   if (piped && ctx->frameNo >= (unsigned long long)nCol && !(S == ctx->stream && ctx->lastMixStream == S))

@@ -30,7 +30,7 @@ PROBE_FRAMES = 90  # bench.py's: the renderer's policy probe after a restart run
 
 
 def per_call(config: str, calls: int = 100, warmup: int = 10, flags: int = 0, device: int = 0,
-             scene=None) -> dict:
+             scene=None, split: bool = False) -> dict:
     cfg, tris, nodes, hdr = scene if scene is not None else scenes.build_config(config)
     eye, rot = orbit_camera(*cfg.camera)
     with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=device,
@@ -48,17 +48,23 @@ def per_call(config: str, calls: int = 100, warmup: int = 10, flags: int = 0, de
         r.reset_stats()
         if os.environ.get("PER_CALL_TRACE"):  # a PT_WAVE_TRACE build records the timed calls' waves only
             os.environ["PT_WAVE_TRACE_FILE"] = os.environ["PER_CALL_TRACE"]
-        ms = []
+        ms, issue = [], []
         for _ in range(calls):
             t0 = time.perf_counter()
-            r.render_frame(eye, rot, f)
+            if split:  # the call's two halves: issuing the frame, then waiting for it (pt_synchronize)
+                r.render_frame(eye, rot, f, sync=False)
+                issue.append(1e3 * (time.perf_counter() - t0))
+                r.synchronize()
+            else:
+                r.render_frame(eye, rot, f)
             ms.append(1e3 * (time.perf_counter() - t0))
             f += 1
         st = r.stats()
     ms.sort()
     med = statistics.median(ms)
     rays = st.rays / max(st.frames, 1)
-    return {"config": config, "calls": calls, "warmup": warmup, "median_ms": round(med, 4),
+    extra = {"issue_ms_median": round(statistics.median(issue), 4)} if split else {}
+    return {**extra, "config": config, "calls": calls, "warmup": warmup, "median_ms": round(med, 4),
             "p10_ms": round(ms[len(ms) // 10], 4), "p90_ms": round(ms[(9 * len(ms)) // 10], 4),
             "min_ms": round(ms[0], 4), "kernel_ms": round(st.kernel_ms_total / max(st.launches, 1), 4),
             "rays_per_frame": int(rays), "mrays_per_s": round(rays / (med * 1e-3) / 1e6, 1),
@@ -106,6 +112,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--analyze", default=None, help="a rocprofv3 kernel-trace directory of this script")
+    ap.add_argument("--split", action="store_true", help="time the issue and the wait of each call apart")
     a = ap.parse_args()
     if os.environ.get("PT_VARIANT"):  # an in-tree diagnostics / tuning build (tools/tune.py --build)
         from opengl_ray_tracing_amd import _native
@@ -114,7 +121,7 @@ def main():
         analyze(a.analyze)
         return
     for c in a.configs:
-        print(json.dumps(per_call(c, a.calls, a.warmup, a.flags)), flush=True)
+        print(json.dumps(per_call(c, a.calls, a.warmup, a.flags, split=a.split)), flush=True)
 
 
 if __name__ == "__main__":
