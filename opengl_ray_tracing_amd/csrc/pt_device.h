@@ -321,9 +321,6 @@ __device__ __forceinline__ float2 hdrCacheTexel(const Env& e, float xi1, float x
   if (e.nt) return e.cache4 ? decodeCache4(ldStream(e.cache4 + k), e.w, e.h) : ldStream(e.cache + k);
   return e.cache4 ? decodeCache4(e.cache4[k], e.w, e.h) : e.cache[k];
 }
-#ifndef PT_ENV_TRIG
-#define PT_ENV_TRIG 1  // SampleHdr's sines and cosines from Env::trig when the table is compact
-#endif
 // SampleHdr's angles of a sample-table entry (x, y), IS:576-580
 __device__ __forceinline__ float hdrTheta(float y) { return PT_PI * ((1.0f - y) - 0.5f); }
 __device__ __forceinline__ float hdrPhi(float x) { return 2.0f * PT_PI * (x - 0.5f); }
@@ -337,7 +334,7 @@ __device__ __forceinline__ V3 sampleHdrDir(const Env& e, float xi1, float xi2, i
   // A compact sample table's entries are integers over (w, h) (decodeCache4), so SampleHdr's sines
   // and cosines take w + h values: Env::trig holds them (envTrigKernel, the same functions of the
   // same floats), one 8-byte load per angle instead of a double-precision sincos each
-  if (PT_ENV_TRIG && e.trig && (e.cacheRow || e.cache4)) {
+  if (e.trig && (e.cacheRow || e.cache4)) {
     int col, row;
     texXY(e.w, e.h, xi1, xi2, col, row);
     uint32_t v;
@@ -411,7 +408,7 @@ __device__ __forceinline__ void hdrColorPdf(const Env& e, V3 L, V3& color, float
 // came from a compact table's entry (sampleHdrDir's *entry) -- the texel's RGBE and the finished pdf,
 // computed at upload by envLightKernel with the operations below -- else computed
 __device__ __forceinline__ void hdrLightColorPdf(const Env& e, int entry, V3 L, V3& color, float& pdf) {
-  if (PT_ENV_TRIG && entry >= 0 && e.light) {
+  if (entry >= 0 && e.light) {
     const float4 c = decodeHdr8(e.nt ? ldStream(e.light + entry) : e.light[entry]);
     color = v3(c.x, c.y, c.z);
     pdf = c.w;
