@@ -43,6 +43,11 @@ constexpr int WIDE_WAVES = 3;
 #endif
 constexpr int WIDE_REGEN_WAVES = PT_WIDE_REGEN_WAVES;
 constexpr int wideRegenWaves(int integrator) { return integrator == 2 ? PT_WIDE_REGEN_WAVES : PT_WIDE_REGEN_WAVES_U; }
+// the MIS wide kernel on scenes that fit the L2s (c3): 3 waves per SIMD, no spills (143 VGPRs), against 4
+// with 9 spilled -- c3 0.1262 -> 0.1216 ms per frame; large scenes keep 4 (c5 4.44 vs 4.79 ms at 3)
+#ifndef PT_WIDE_REGEN_WAVES_SMALL
+#define PT_WIDE_REGEN_WAVES_SMALL 3
+#endif
 #ifndef PT_MIN_WAVES
 #define PT_MIN_WAVES 1            // __launch_bounds__ minimum waves per SIMD of the render kernels
 #endif
@@ -389,15 +394,17 @@ hipError_t launchPrimary(const RenderParams& p, hipStream_t s);
 struct RegenShape {
   bool wide = false;      // the large-scene variant (WIDE_REGEN_WAVES, 4-wide walk, dynamic ray fetch)
   bool fullTree = false;  // ... with the whole 4-wide tree in LDS (small trees, uniform integrators)
+  bool small = false;     // the MIS variant at PT_WIDE_REGEN_WAVES_SMALL waves per SIMD (scenes that fit the L2s)
   int block = BLOCK;      // threads per block
   int blocksPerCU = 0;    // resident blocks per CU
   size_t dynLds = 0;      // dynamic LDS bytes per block (the tree)
 };
 // f4nDev: nodes of the 4-wide runtime tree the frame walks (0: it walks none)
-hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenShape* out);
+// smallScene: the scene's records fit the L2s (not a PT_WIDE_SCENE_MB scene)
+hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, bool smallScene, RegenShape* out);
 hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStream_t s, bool cull, const RegenShape& r);
 int regenLdsStack();
-int regenTop4(int integrator);  // 4-wide nodes the wide regen kernel stages in LDS (PT_REGEN_TOP4[_3])
+int regenTop4(const RegenShape& r, int integrator);  // 4-wide nodes the wide regen kernel stages in LDS (PT_REGEN_TOP4[_3])
 hipError_t launchTrace(const TraceParams& p, int grid, hipStream_t s, bool cull);
 hipError_t launchBasic(const BasicParams& p, hipStream_t s);
 // BASIC checkpoints: the double image from the f32 sums (widened), or the f32 sums from the double image

@@ -643,15 +643,18 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
 constexpr int FULL_BS = 256 * PT_WIDE_REGEN_WAVES_U;  // one block per CU: all its waves share the tree
 constexpr size_t LDS_BYTES = 160 * 1024;
 template <int I>
-static const void* regenFn(bool cull, bool wide, bool full) {
+static const void* regenFn(bool cull, bool wide, bool full, bool small) {
   if constexpr (I != 2 && PT_REGEN_YIELD > 0)  // the uniform integrators' variant only
     if (full) return (const void*)regenKernel<I, true, wideRegenWaves(I), true, FULL_BS, true>;
+  if constexpr (I == 2 && PT_WIDE_REGEN_WAVES_SMALL != PT_WIDE_REGEN_WAVES)
+    if (wide && small) return (const void*)regenKernel<I, true, PT_WIDE_REGEN_WAVES_SMALL, true>;
   if (wide) return (const void*)regenKernel<I, true, wideRegenWaves(I), true>;
   return cull ? (const void*)regenKernel<I, true> : (const void*)regenKernel<I, false>;
 }
-static const void* regenFnI(int integrator, bool cull, bool wide, bool full) {
-  return integrator == 0 ? regenFn<0>(cull, wide, full) : integrator == 1 ? regenFn<1>(cull, wide, full)
-                                                                         : regenFn<2>(cull, wide, full);
+static const void* regenFnI(int integrator, bool cull, bool wide, bool full, bool small = false) {
+  return integrator == 0   ? regenFn<0>(cull, wide, full, small)
+         : integrator == 1 ? regenFn<1>(cull, wide, full, small)
+                           : regenFn<2>(cull, wide, full, small);
 }
 
 static long long fullStaticLds(int integrator) {
@@ -660,9 +663,10 @@ static long long fullStaticLds(int integrator) {
   return (long long)fa.sharedSizeBytes;
 }
 
-hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenShape* out) {
+hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, bool smallScene, RegenShape* out) {
   RegenShape r;
   r.wide = wide && cull;
+  r.small = integrator == 2 && r.wide && smallScene && PT_WIDE_REGEN_WAVES_SMALL != PT_WIDE_REGEN_WAVES;
   const size_t treeBytes = (size_t)f4nDev * W4_LDS_F4 * sizeof(float4);
   // the FULL variant's static LDS (stack rows, hand-out rows, phase counters) as compiled
   // (a property of the code object, the same on every device: read once per integrator)
@@ -678,7 +682,7 @@ hipError_t regenShape(int integrator, bool cull, bool wide, int f4nDev, RegenSha
                treeBytes + staticBytes <= LDS_BYTES;
   r.block = r.fullTree ? FULL_BS : BLOCK;
   r.dynLds = r.fullTree ? treeBytes : 0;
-  const void* f = regenFnI(integrator, cull, r.wide, r.fullTree);
+  const void* f = regenFnI(integrator, cull, r.wide, r.fullTree, r.small);
   if (r.fullTree) {
     // room for any tree that fits beside the static LDS; a function attribute is per device, and
     // setting it is cheap, so every shape query on the current device sets it
@@ -700,6 +704,11 @@ static hipError_t launchRegenI(const RenderParams& p, int grid, hipStream_t s, b
     }
   }
   if (r.fullTree) return hipErrorInvalidValue;
+  if constexpr (I == 2 && PT_WIDE_REGEN_WAVES_SMALL != PT_WIDE_REGEN_WAVES)
+    if (r.wide && r.small) {
+      hipLaunchKernelGGL((regenKernel<I, true, PT_WIDE_REGEN_WAVES_SMALL, true>), dim3(grid), dim3(BLOCK), 0, s, p);
+      return hipGetLastError();
+    }
   if (r.wide)
     hipLaunchKernelGGL((regenKernel<I, true, wideRegenWaves(I), true>), dim3(grid), dim3(BLOCK), 0, s, p);
   else if (cull) hipLaunchKernelGGL((regenKernel<I, true>), dim3(grid), dim3(BLOCK), 0, s, p);
@@ -717,6 +726,8 @@ hipError_t launchRegen(const RenderParams& p, int integrator, int grid, hipStrea
 }
 
 int regenLdsStack() { return REGEN_LDS_STACK; }
-int regenTop4(int integrator) { return regenTop4W(wideRegenWaves(integrator)); }
+int regenTop4(const RegenShape& r, int integrator) {
+  return regenTop4W(r.small ? PT_WIDE_REGEN_WAVES_SMALL : wideRegenWaves(integrator));
+}
 
 }  // namespace pt

@@ -1679,7 +1679,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   const bool walk4 = wide && ctx->fast4Ready && !(c.flags & PT_FLAG_REFERENCE_TREE);
   RegenShape rs;
   if (regen) {
-    CK(regenShape(c.integrator, cull, wide, walk4 ? ctx->f4nDev : 0, &rs));
+    CK(regenShape(c.integrator, cull, wide, walk4 ? ctx->f4nDev : 0, !wideScene, &rs));
     nb = rs.blocksPerCU;
   } else {
     CK(renderBlocksPerCU(c.integrator, cull, count, wide, &nb));
@@ -1803,7 +1803,7 @@ static int renderOne(pt_ctx* ctx, const float eye[3], const float cameraRotate[1
   // the large-scene regen kernel walks the 4-wide runtime tree (checked against the uploaded one)
   if (regen && walk4) useFast = true;
   if (regen && wide)  // its own LDS copy's size: the top of the tree, or all of it
-    p.scene.f4nTop = rs.fullTree ? ctx->f4nDev : std::min(regenTop4(c.integrator), ctx->f4nDev);
+    p.scene.f4nTop = rs.fullTree ? ctx->f4nDev : std::min(regenTop4(rs, c.integrator), ctx->f4nDev);
   p.scene.fast = useFast ? 1 : 0;
   ctx->lastFast = useFast;
   // While the policy probe times frames (PT_SPLIT_AUTO, 20 frames after a restart) a pipelined

@@ -165,6 +165,8 @@ def test_frame_kernels_agree(request, name, integrator):
     # bounces (pt_runtime.cpp regenAll); a synchronous display() call's single frame the megakernel
     assert sb.regen == 0 and sd.regen == 0
     assert se.regen == (1 if integrator == "lambert" or (integrator == "mis" and mb <= 2) else 0)
+    if integrator == "mis" and se.regen:  # the MIS wide kernel on a scene that fits the L2s: 3 waves/SIMD
+        assert se.waves_per_simd == 3
     assert np.array_equal(a, b)
     assert np.array_equal(d, b)
     assert np.array_equal(e, b)
