@@ -29,6 +29,37 @@ from opengl_ray_tracing_amd import Renderer, orbit_camera, scenes  # noqa: E402
 PROBE_FRAMES = 90  # bench.py's: the renderer's policy probe after a restart runs before the timed calls
 
 
+def queued(config: str, calls: int = 100, depth: int = 2, flags: int = 0, device: int = 0) -> dict:
+    """display() calls that do not wait for their frame, as a GL program's do (glutSwapBuffers returns
+    while the driver holds a few frames): pt_render_frame_async per call, pt_synchronize every `depth`
+    calls (a queue of at most `depth` frames). Reports the mean wall time per call."""
+    cfg, tris, nodes, hdr = scenes.build_config(config)
+    eye, rot = orbit_camera(*cfg.camera)
+    with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, device=device,
+                  flags=flags) as r:
+        r.upload_scene(tris, nodes)
+        r.upload_env(hdr)
+        f = 0
+        for _ in range(PROBE_FRAMES + 10):
+            r.render_frame(eye, rot, f, sync=False)
+            f += 1
+        r.synchronize()
+        r.reset_stats()
+        t0 = time.perf_counter()
+        for k in range(calls):
+            r.render_frame(eye, rot, f, sync=False)
+            f += 1
+            if (k + 1) % depth == 0:
+                r.synchronize()
+        r.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / calls
+        st = r.stats()
+    rays = st.rays / max(st.frames, 1)
+    return {"config": config, "calls": calls, "queue_depth": depth, "ms_per_call": round(ms, 4),
+            "mrays_per_s": round(rays / (ms * 1e-3) / 1e6, 1),
+            "frame_kernel": "path regeneration" if st.regen else "lock-step megakernel"}
+
+
 def per_call(config: str, calls: int = 100, warmup: int = 10, flags: int = 0, device: int = 0,
              scene=None, split: bool = False) -> dict:
     cfg, tris, nodes, hdr = scene if scene is not None else scenes.build_config(config)
@@ -113,6 +144,7 @@ def main():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--analyze", default=None, help="a rocprofv3 kernel-trace directory of this script")
     ap.add_argument("--split", action="store_true", help="time the issue and the wait of each call apart")
+    ap.add_argument("--queue", type=int, default=0, help="calls that wait only every QUEUE frames (queued())")
     a = ap.parse_args()
     if os.environ.get("PT_VARIANT"):  # an in-tree diagnostics / tuning build (tools/tune.py --build)
         from opengl_ray_tracing_amd import _native
@@ -121,7 +153,10 @@ def main():
         analyze(a.analyze)
         return
     for c in a.configs:
-        print(json.dumps(per_call(c, a.calls, a.warmup, a.flags, split=a.split)), flush=True)
+        if a.queue:
+            print(json.dumps(queued(c, a.calls, a.queue, a.flags)), flush=True)
+        else:
+            print(json.dumps(per_call(c, a.calls, a.warmup, a.flags, split=a.split)), flush=True)
 
 
 if __name__ == "__main__":
