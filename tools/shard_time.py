@@ -9,7 +9,8 @@ on the render stream, and the one-launch unpack of the other N - 1 ranks' buffer
 accumulation on the communication stream) but no collective (PT_SHARD_GATHER=0: render only).
 The N-GPU frame is this plus whatever of the xGMI gather itself does not overlap the next batch.
 
-    [PT_VARIANT=<tuning build>] [PT_BATCH=b | PT_BATCH_MUL=m] [PT_SHARD_FRAMES=K] python tools/shard_time.py [config] [N ...]
+    [PT_VARIANT=<tuning build>] [PT_BATCH=b | PT_BATCH_MUL=m] [PT_SHARD_FRAMES=K] [PT_SHARD_FLAGS=f]
+        python tools/shard_time.py [config] [N ...]
 """
 import json
 import sys
@@ -40,7 +41,8 @@ def main():
     with_gather = os.environ.get("PT_SHARD_GATHER", "1") != "0"
     for n in worlds:
         with Renderer(cfg.width, cfg.height, cfg.integrator, max_bounce=cfg.max_bounce, tile_rank=0,
-                      tile_world=n, frame_batch=mul * n if mul else batch) as r:
+                      tile_world=n, frame_batch=mul * n if mul else batch,
+                      flags=int(os.environ.get("PT_SHARD_FLAGS", "0"), 0)) as r:
             r.upload_scene(tris, nodes)
             r.upload_env(hdr)
             g = FrameGather(r, 0, n, "cuda:0", mode="accum", proxy=True,
