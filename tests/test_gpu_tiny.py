@@ -63,3 +63,36 @@ def test_single_triangle_scene_equals_oracle():
         streamed, called, ref = render_both(48, 40, integrator, tris, nodes, hdr, eye, rot)
         assert np.isfinite(ref).all()
         assert np.array_equal(streamed, ref) and np.array_equal(called, ref), integrator
+
+
+@pytest.mark.parametrize("integrator", ["lambert", "mis"])
+def test_screen_tile_ranks_without_tiles(integrator):
+    """More ranks than 32x32 screen tiles (a 40x40 window split 8 ways: 4 tiles): the ranks that own
+    no tile render nothing, without error; the others' tiles equal the oracle's image."""
+    cfg, tris, nodes, hdr = scenes.build_config("c2")
+    eye, rot = orbit_camera(*cfg.camera)
+    w = h = 40
+    o = oracle.Oracle(tris, nodes, hdr)
+    ref = np.zeros((h, w, 4), np.float32)
+    for f in range(FRAMES):
+        ref, _ = o.render(w, h, integrator, f, eye, rot, accum=ref, max_bounce=2)
+    world = 8
+    covered = np.zeros((h, w), bool)
+    for rank in range(world):
+        with Renderer(w, h, integrator, max_bounce=2, tile_rank=rank, tile_world=world) as r:
+            r.upload_scene(tris, nodes)
+            r.upload_env(hdr)
+            r.render_frames(eye, rot, 0, FRAMES - 1)
+            r.render_frame(eye, rot, FRAMES - 1)
+            a = r.accum()
+            n = r.owned_pixel_count()
+        mine = np.zeros((h, w), bool)
+        owned = range(rank, 4, world)  # shard tiles t (row-major, 2 x 2 of them)
+        for t in owned:
+            ty, tx = divmod(t, 2)
+            mine[32 * ty:32 * ty + 32, 32 * tx:32 * tx + 32] = True
+        assert n == 32 * 32 * len(owned)  # packed slots: whole shard tiles
+        assert np.array_equal(a[mine], ref[mine])
+        assert not a[~mine].any()
+        covered |= mine
+    assert covered.all()
