@@ -587,7 +587,9 @@ __global__ __launch_bounds__(BS, WAVES > 0 ? WAVES : (INTEG == 2 ? PT_REGEN_MIN_
 #endif
       t = w.tbest;
       tri = w.best;
-      const bool retrace = w.tie || (tri >= 0 && !refReachable(p.scene, tri, s.o, s.d, t));
+      // (the MIS kernel of the large scenes, whose reference trees are deep: the walk up stops early)
+      const bool retrace =
+          w.tie || (tri >= 0 && !refReachable<INTEG == 2 && WAVES == PT_WIDE_REGEN_WAVES>(p.scene, tri, s.o, s.d, t));
       PH_ADD(14, __popcll(__ballot(retrace)));
       if (retrace) {
         C.rays--;  // the same ray, counted once
